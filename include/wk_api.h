@@ -1,0 +1,230 @@
+/*
+ * wk_api.h -- C ABI of the MI355X-native batched bipedal-walker physics + PPO engine.
+ *
+ * Drop-in boundary for the reference's hot path (De-Rosa/PPO-BipedalWalker, C#).  The
+ * reference has no FFI of its own; these entry points replace the managed calls that
+ * sit on the path (citations are /root/reference file:line):
+ *
+ *   wk_create / wk_destroy     Environment ctor (Environment.cs:39-51), Walker ctor
+ *                              (Walker/Walker.cs:25-46), PPOAgent ctor (PPOAgent.cs:23-37),
+ *                              CreateFloor (Environment.cs:211-226)
+ *   wk_step                    Environment.Update (Environment.cs:64-92): SampleActions
+ *                              (PPOAgent.cs:381-398) or caller actions, Clip (:78),
+ *                              Walker.TakeActions/Joint.SetTorque (Walker.cs:66-75,
+ *                              Joint.cs:56-61), StepObjects (Environment.cs:126-143:
+ *                              Joint.Step Joint.cs:31-41 + IObject.Update Objects/IObject.cs:9
+ *                              -> RigidBody.Step Bodies/RigidBody.cs:54-61), Walker.Update
+ *                              (Walker.cs:49-54), CalculateReward (Environment.cs:148-154),
+ *                              terminal (:106-117), GetState (Walker.cs:132-152),
+ *                              auto Reset (Environment.cs:167-180)
+ *   wk_reset                   Environment.Reset / Walker.Reset (Environment.cs:167-173,
+ *                              Walker.cs:212-223)
+ *   wk_set_materials           Walker._material : IMaterial (Walker.cs:17,30; Materials/<Name>.cs)
+ *   wk_get_body_view           RigidBody.GetVectors/GetCentroid/... for Renderer and
+ *                              ConsoleRenderer (Bodies/RigidBody.cs:191-261)
+ *   wk_policy_sample           PPOAgent.SampleActions (PPOAgent.cs:381-398)
+ *   wk_value                   PPOAgent.GetValueEstimate (PPOAgent.cs:350-364)
+ *   wk_rollout                 Environment.Update x horizon with Trajectory recording
+ *                              (Environment.cs:71-89, Trajectory.cs:7-50) + CalculateValues
+ *                              (PPOAgent.cs:175-189)
+ *   wk_ppo_update              PPOAgent.Train(Trajectory) (PPOAgent.cs:147-172): CreateBatches
+ *                              (:501-540), Train(Batch) (:218-346), NeuralNetwork.Optimise /
+ *                              DenseLayer.Adam (NeuralNetwork.cs:85-91, DenseLayer.cs:125-159)
+ *   wk_train_batch             PPOAgent.Train(Batch) on caller data (parity entry)
+ *   wk_get/set_weights         NeuralNetwork.Save/Load (NeuralNetwork.cs:94-115,159-176),
+ *                              flat fp32, critic layers then actor layers, each W (out x in,
+ *                              row-major) then B -- the .weights order (DenseLayer.cs:73-79)
+ *   wk_comm_*                  (new) RCCL all-reduce of policy gradients across GPUs
+ *
+ * Conventions: every call returns 0 on success or a negative wk_status; the text is
+ * in wk_last_error(ctx).  The C# side forwards it to ErrorLogger.LogError and
+ * continues (the reference's log-and-continue convention, Rendering/ErrorLogger.cs:42-78).
+ * Per-env soft faults (non-finite state, skipped PPO samples) are reported as bitmasks,
+ * never as errors.  Host arrays are caller-owned, borrowed for the call and copied;
+ * *_device variants take device pointers on the context's stream.  A context is not
+ * thread-safe: one host thread per context / GPU.
+ */
+#ifndef WK_API_H
+#define WK_API_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct wk_ctx wk_ctx;
+
+enum wk_status {
+  WK_OK = 0,
+  WK_ERR_ARG = -1,       /* invalid argument */
+  WK_ERR_HIP = -2,       /* HIP runtime error */
+  WK_ERR_CONFIG = -3,    /* unsupported configuration (e.g. non-default network DSL) */
+  WK_ERR_COMM = -4,      /* RCCL error */
+  WK_ERR_STATE = -5      /* call order (e.g. ppo_update before rollout) */
+};
+
+/* per-env fault bits (wk_step fault[] / wk_rollout) */
+enum wk_fault { WK_FAULT_NONFINITE = 1u, WK_FAULT_SKIPPED_SAMPLE = 2u };
+
+/* materials: Materials/<Name>.cs */
+enum wk_material {
+  WK_MAT_CARPET = 0, WK_MAT_ICE = 1, WK_MAT_RUBBER = 2, WK_MAT_METAL = 3, WK_MAT_WOOD = 4,
+  WK_MAT_PAPER = 5, WK_MAT_TITANIUM = 6, WK_MAT_SUPERRUBBER = 7
+};
+
+/* Hyperparameters (Walker/PPO/Hyperparameters.cs:80-121): same names and defaults.
+ * Batched extensions are marked (new). */
+typedef struct wk_config {
+  int GameSpeed;            /* 1 (UI only; ignored) */
+  int Iterations;           /* 50 physics substeps per env-step */
+  int MaxTimesteps;         /* 1000 */
+  int RoughFloor;           /* 0 (1 is rejected: SURVEY 8(f) next-3) */
+  int Epochs;               /* 5 */
+  int BatchSize;            /* 64 */
+  int UseGAE;               /* 0 */
+  int NormalizeAdvantages;  /* 0 */
+  float Gamma;              /* 0.9 */
+  float Lambda;             /* 0.95 */
+  float Epsilon;            /* 0.3 */
+  float LogStandardDeviation; /* -1 */
+  float Alpha;              /* 1e-3 */
+  float Beta1;              /* 0.9 */
+  float Beta2;              /* 0.999 */
+  float AdamEpsilon;        /* 1e-8 */
+  const char* CriticNeuralNetwork; /* NULL or "Input |64| (LeakyReLU) |1| Output" */
+  const char* ActorNeuralNetwork;  /* NULL or "Input |64| (LeakyReLU) |64| (LeakyReLU) |4| (TanH) Output" */
+  float DeltaTime;          /* MonoGame fixed step, (float)(166667 ticks / 1e7) */
+  /* (new) batched extensions */
+  int Horizon;              /* rollout horizon T_h of the device trajectory buffer (64) */
+  int Minibatch;            /* local minibatch M for wk_ppo_update (0 -> BatchSize) */
+  int MinibatchGlobal;      /* divisor of dV/dmu = global minibatch (0 -> Minibatch * nranks) */
+  int EnvOffset;            /* global id of this context's env 0 (Philox streams) */
+  int RandomizeStart;       /* 1: env e starts at x + 200*u_e (BASELINE config 2) */
+  int RandomizeMaterial;    /* 1: env material in {Ice, Rubber, Carpet} (config 5) */
+} wk_config;
+
+/* canonical per-env state dump: WK_STATE_FLOATS floats per env (identical layout to
+ * the oracle's orc_env_dump).  Body b in {LLL, LLU, BODY, RLL, RLU} at b*20:
+ * verts x0,y0..x5,y5 (BODY uses 5), centroid x,y, v x,y, w, angle, collided, pad. */
+enum {
+  WK_STATE_FLOATS = 112, WK_ST_TORQUE = 100, WK_ST_POS = 104, WK_ST_PREV = 106,
+  WK_ST_STEPS = 108, WK_ST_POSTRESET = 109, WK_ST_TERMINAL = 110, WK_ST_EPISODES = 111,
+  WK_NPARAM_CRITIC = 897, WK_NPARAM_ACTOR = 5252, WK_NPARAM = 6149, WK_OBS = 12, WK_ACT = 4,
+  WK_NPAIRS = 9
+};
+
+/* per-substep pair bookkeeping (bit-exact parity outputs).  Canonical
+ * pair index: 0 (LLL,LLU) 1 (LLL,FLOOR) 2 (LLU,LLL) 3 (LLU,FLOOR) 4 (BODY,FLOOR)
+ * 5 (RLL,RLU) 6 (RLL,FLOOR) 7 (RLU,RLL) 8 (RLU,FLOOR). */
+typedef struct wk_pair_trace {
+  uint8_t aabb_hit[WK_NPAIRS];
+  uint8_t sat_hit[WK_NPAIRS];
+  uint8_t n_contacts[WK_NPAIRS];
+  uint8_t pad[5];
+  float normal[WK_NPAIRS][2];
+  float depth[WK_NPAIRS];
+} wk_pair_trace;
+
+/* one body of one env, for Renderer.RenderRigidObject / ConsoleRenderer */
+typedef struct wk_body_view {
+  int n_vertices;
+  float vertices[6][2];
+  float centroid[2];
+  float linear_velocity[2];
+  float angular_velocity;
+  float angle;
+  int collided;
+  int is_static;
+} wk_body_view;
+
+typedef struct wk_ppo_args {
+  int epochs;          /* 0 -> config Epochs */
+  int minibatch;       /* 0 -> config Minibatch */
+  int minibatch_global;/* 0 -> config MinibatchGlobal */
+  uint32_t update_index; /* permutation key: minibatch sampling of update #k */
+} wk_ppo_args;
+
+typedef struct wk_rollout_stats {
+  double reward_sum;     /* sum of rewards over the horizon, this context */
+  int64_t episodes;      /* terminal steps in the horizon */
+  int64_t env_steps;     /* n_env * horizon */
+  uint32_t fault_or;     /* OR of per-env fault bits */
+  int32_t pad;
+} wk_rollout_stats;
+
+/* kernel timing (HIP events on the context's stream), cumulative since last reset */
+typedef struct wk_profile {
+  double physics_ms;   int64_t physics_launches;  int64_t physics_env_steps;
+  double grad_ms;      int64_t grad_launches;
+  double reduce_ms;    int64_t reduce_launches;
+  double adam_ms;      int64_t adam_launches;
+  double allreduce_ms; int64_t allreduce_calls;
+  double returns_ms;   int64_t returns_launches;
+} wk_profile;
+
+void wk_config_defaults(wk_config* cfg);
+const char* wk_version(void);
+
+int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx** out);
+int wk_destroy(wk_ctx* ctx);
+const char* wk_last_error(const wk_ctx* ctx); /* ctx may be NULL (create errors) */
+int wk_sync(wk_ctx* ctx);
+int wk_num_envs(const wk_ctx* ctx);
+
+/* environment */
+int wk_reset(wk_ctx* ctx, const uint8_t* mask /* n_env or NULL = all */);
+int wk_set_materials(wk_ctx* ctx, const int32_t* mat_id /* n_env */);
+int wk_set_offsets(wk_ctx* ctx, const float* dx /* n_env; start x = 125 + dx */);
+int wk_step(wk_ctx* ctx, const float* actions_or_null /* k*n_env*4, unclipped */, int k_steps,
+            float* obs /* k*n_env*12 or NULL */, float* reward /* k*n_env or NULL */,
+            uint8_t* done /* k*n_env or NULL */, uint32_t* fault /* n_env or NULL */);
+int wk_step_device(wk_ctx* ctx, const float* d_actions_or_null, int k_steps, float* d_obs,
+                   float* d_reward, uint8_t* d_done, uint32_t* d_fault);
+/* one env-step with per-substep pair bookkeeping: trace[n_env * Iterations] */
+int wk_step_traced(wk_ctx* ctx, const float* actions /* n_env*4 */, wk_pair_trace* trace);
+int wk_get_obs(wk_ctx* ctx, float* obs /* n_env*12 */);
+int wk_get_state(wk_ctx* ctx, float* state /* n_env*WK_STATE_FLOATS */);
+int wk_set_state(wk_ctx* ctx, const float* state /* n_env*WK_STATE_FLOATS */);
+int wk_get_body_view(wk_ctx* ctx, int env, int body /* 0..4 walker, 5 floor */, wk_body_view* out);
+
+/* policy / value */
+int wk_get_weights(wk_ctx* ctx, float* params /* WK_NPARAM */);
+int wk_set_weights(wk_ctx* ctx, const float* params);
+int wk_get_adam(wk_ctx* ctx, float* m, float* v, int* t);
+int wk_set_adam(wk_ctx* ctx, const float* m, const float* v, int t);
+int wk_policy_sample(wk_ctx* ctx, int n, const float* obs /* n*12 */, const int32_t* env_ids,
+                     const uint32_t* steps, float* mean, float* act, float* logp);
+int wk_value(wk_ctx* ctx, int n, const float* obs, float* v);
+
+/* rollout + PPO (device-resident trajectory buffer [Horizon][n_env]) */
+int wk_rollout(wk_ctx* ctx, int horizon /* <= config Horizon; 0 = Horizon */);
+int wk_rollout_stats_get(wk_ctx* ctx, wk_rollout_stats* out);
+int wk_get_trajectory(wk_ctx* ctx, float* states, float* actions, float* logp, float* rewards,
+                      uint8_t* dones, float* values, float* returns, float* advantages);
+int wk_set_trajectory(wk_ctx* ctx, int horizon, const float* states, const float* actions,
+                      const float* logp, const float* rewards, const uint8_t* dones,
+                      const float* values);
+int wk_compute_returns(wk_ctx* ctx);
+int wk_ppo_update(wk_ctx* ctx, const wk_ppo_args* args, float* critic_diag, float* actor_diag);
+/* Train(Batch) on caller data: B samples, divisor b_div; grads_out (optional, WK_NPARAM)
+ * receives the accumulated gradient before Adam. Returns skipped-sample count in *skipped. */
+int wk_train_batch(wk_ctx* ctx, int B, float b_div, const float* states, const float* actions,
+                   const float* logp_old, const float* returns, const float* adv,
+                   float* critic_diag, float* actor_diag, float* grads_out, int apply_adam,
+                   int* skipped);
+
+/* multi-GPU: RCCL communicator over the ranks' contexts (one per GPU) */
+int wk_comm_unique_id(uint8_t* id /* 128 bytes */);
+int wk_comm_init(wk_ctx* ctx, int rank, int nranks, const uint8_t* unique_id);
+int wk_allreduce_test(wk_ctx* ctx, float* host_buf, int n); /* sum in place (tests) */
+
+/* profiling */
+int wk_profile_enable(wk_ctx* ctx, int on);
+int wk_profile_get(wk_ctx* ctx, wk_profile* out);
+int wk_profile_reset(wk_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,826 @@
+// wk_api.cpp -- C-ABI implementation (include/wk_api.h): context, device memory,
+// launches on the context's HIP stream, RCCL gradient all-reduce, kernel timing.
+//
+// Host responsibilities only: argument validation (Hyperparameters validation,
+// Walker/PPO/Hyperparameters.cs:189-217), buffer management, the per-minibatch launch
+// sequence of PPOAgent.Train(Trajectory) (PPOAgent.cs:147-172) and the double-precision
+// Adam bias corrections (DenseLayer.cs:142-145: (float)(1 - Math.Pow(beta, t))).
+// Every compute step runs in a HIP kernel; there is no CPU fallback.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/wk_api.h"
+#include "wk_common.h"
+#include "wk_kernels.h"
+
+
+static const char* kCriticDefault = "Input |64| (LeakyReLU) |1| Output";
+static const char* kActorDefault = "Input |64| (LeakyReLU) |64| (LeakyReLU) |4| (TanH) Output";
+static thread_local std::string g_create_error;
+
+enum ProfKind { PK_PHYS = 0, PK_GRAD, PK_REDUCE, PK_ADAM, PK_ALLRED, PK_RET, PK_N };
+
+struct wk_ctx {
+  wk_config cfg;
+  int device = 0;
+  int n = 0;
+  uint64_t seed = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  wk::EnvParams P{};
+  float lp_const = 0.0f;
+  // env
+  float* st = nullptr;        // [NSTATE][n]
+  float* dxoff = nullptr;     // [n]
+  int32_t* mat = nullptr;     // [n]
+  uint32_t* rng_t = nullptr;  // [n]
+  // params
+  float* W = nullptr; float* m = nullptr; float* v = nullptr; float* grad = nullptr;
+  int adam_t = 0;
+  // trajectory [T][n]
+  int T = 0, T_valid = 0;
+  float *ts = nullptr, *ta = nullptr, *tlp = nullptr, *tr = nullptr, *tv = nullptr, *tret = nullptr, *tadv = nullptr;
+  uint8_t* td = nullptr;
+  bool returns_valid = false;
+  // scratch
+  float* partial = nullptr; size_t partial_floats = 0;
+  void* scratch = nullptr; size_t scratch_bytes = 0;
+  void* scratch2 = nullptr; size_t scratch2_bytes = 0;
+  // comm
+  ncclComm_t comm = nullptr;
+  int rank = 0, nranks = 1;
+  // profiling
+  bool prof = false;
+  struct Ev { int kind; hipEvent_t a, b; int64_t units; };
+  std::vector<Ev> pending;
+  std::vector<hipEvent_t> pool;
+  double prof_ms[PK_N] = {0};
+  int64_t prof_cnt[PK_N] = {0};
+  int64_t prof_units = 0;
+};
+
+#define SETERR(ctx, ...)                                           \
+  do {                                                             \
+    char _b[512];                                                  \
+    snprintf(_b, sizeof(_b), __VA_ARGS__);                         \
+    (ctx)->err = _b;                                               \
+  } while (0)
+
+#define HIPCHK(ctx, call)                                                               \
+  do {                                                                                  \
+    hipError_t _e = (call);                                                             \
+    if (_e != hipSuccess) {                                                             \
+      SETERR(ctx, "%s failed: %s (%s:%d)", #call, hipGetErrorString(_e), __FILE__, __LINE__); \
+      return WK_ERR_HIP;                                                                \
+    }                                                                                   \
+  } while (0)
+
+static hipEvent_t ev_get(wk_ctx* c) {
+  if (!c->pool.empty()) {
+    hipEvent_t e = c->pool.back();
+    c->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+struct ProfScope {
+  wk_ctx* c; int kind; int64_t units; hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(wk_ctx* c_, int k, int64_t u = 0) : c(c_), kind(k), units(u) {
+    if (c->prof) {
+      a = ev_get(c); b = ev_get(c);
+      if (a) hipEventRecord(a, c->stream);
+    }
+  }
+  ~ProfScope() {
+    if (c->prof && a && b) {
+      hipEventRecord(b, c->stream);
+      c->pending.push_back({kind, a, b, units});
+    }
+  }
+};
+
+static void prof_drain(wk_ctx* c) {
+  for (auto& e : c->pending) {
+    float ms = 0.0f;
+    if (hipEventSynchronize(e.b) == hipSuccess && hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
+      c->prof_ms[e.kind] += ms;
+      c->prof_cnt[e.kind] += 1;
+      if (e.kind == PK_PHYS) c->prof_units += e.units;
+    }
+    c->pool.push_back(e.a);
+    c->pool.push_back(e.b);
+  }
+  c->pending.clear();
+}
+
+static int ensure(wk_ctx* c, void** p, size_t* have, size_t need) {
+  if (*have >= need) return 0;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  HIPCHK(c, hipMalloc(p, need));
+  *have = need;
+  return 0;
+}
+
+extern "C" {
+
+void wk_config_defaults(wk_config* c) {
+  if (!c) return;
+  memset(c, 0, sizeof(*c));
+  c->GameSpeed = 1;
+  c->Iterations = 50;
+  c->MaxTimesteps = 1000;
+  c->RoughFloor = 0;
+  c->Epochs = 5;
+  c->BatchSize = 64;
+  c->UseGAE = 0;
+  c->NormalizeAdvantages = 0;
+  c->Gamma = 0.9f;
+  c->Lambda = 0.95f;
+  c->Epsilon = 0.3f;
+  c->LogStandardDeviation = -1.0f;
+  c->Alpha = 0.001f;
+  c->Beta1 = 0.9f;
+  c->Beta2 = 0.999f;
+  c->AdamEpsilon = 1e-8f;
+  c->CriticNeuralNetwork = nullptr;
+  c->ActorNeuralNetwork = nullptr;
+  c->DeltaTime = (float)(166667.0 / 10000000.0);
+  c->Horizon = 64;
+  c->Minibatch = 0;
+  c->MinibatchGlobal = 0;
+  c->EnvOffset = 0;
+  c->RandomizeStart = 0;
+  c->RandomizeMaterial = 0;
+}
+
+const char* wk_version(void) { return "wk 0.1 (gfx950)"; }
+
+const char* wk_last_error(const wk_ctx* ctx) {
+  return ctx ? ctx->err.c_str() : g_create_error.c_str();
+}
+
+// ValidateHyperparameterValues (Hyperparameters.cs:189-217) + the kernel's fixed shapes
+static int validate(const wk_config* c, std::string& why) {
+  char b[256];
+  auto bad = [&](const char* m) { why = m; return WK_ERR_CONFIG; };
+  if (c->Iterations <= 0 || c->Iterations >= 200) return bad("Invalid iterations count, should be in range 0<x<200");
+  if (c->MaxTimesteps <= 0) return bad("Invalid maximum time steps amount, should be in range x>0");
+  if (c->Alpha <= 0 || c->Alpha >= 10) return bad("Invalid alpha value, should be in range 0<x<10");
+  if (c->Beta1 <= 0 || c->Beta1 > 1) return bad("Invalid beta1 value, should be in range 0<x<1");
+  if (c->Beta2 <= 0 || c->Beta2 > 1) return bad("Invalid beta2 value, should be in range 0<x<1");
+  if (c->AdamEpsilon <= 0 || c->AdamEpsilon >= 1) return bad("Invalid Adam epsilon value, should be in range 0<x<1");
+  if (c->Epochs <= 0 || c->Epochs >= 50) return bad("Invalid epochs value, should be in range 0<x<50");
+  if (c->BatchSize <= 0 || c->BatchSize >= 1000) return bad("Invalid batch size value, should be in range 0<x<1000");
+  if (c->Gamma <= 0 || c->Gamma > 1) return bad("Invalid gamma value, should be in range 0<x<1");
+  if (c->Lambda <= 0 || c->Lambda > 1) return bad("Invalid lambda value, should be in range 0<x<1");
+  if (c->Epsilon <= 0 || c->Epsilon > 1) return bad("Invalid epsilon value, should be in range 0<x<1");
+  if (c->LogStandardDeviation <= -5 || c->LogStandardDeviation >= 5) return bad("Invalid log standard deviation value, should be in range -5<x<5");
+  if (c->RoughFloor) return bad("RoughFloor is not supported by the batched kernel (SURVEY 8(f) next-3)");
+  if (c->CriticNeuralNetwork && strcmp(c->CriticNeuralNetwork, kCriticDefault) != 0) {
+    snprintf(b, sizeof(b), "critic network '%s' unsupported: the kernels implement '%s'", c->CriticNeuralNetwork, kCriticDefault);
+    why = b;
+    return WK_ERR_CONFIG;
+  }
+  if (c->ActorNeuralNetwork && strcmp(c->ActorNeuralNetwork, kActorDefault) != 0) {
+    snprintf(b, sizeof(b), "actor network '%s' unsupported: the kernels implement '%s'", c->ActorNeuralNetwork, kActorDefault);
+    why = b;
+    return WK_ERR_CONFIG;
+  }
+  if (c->Horizon <= 0) return bad("Horizon must be > 0");
+  if (c->Minibatch < 0) return bad("Minibatch must be >= 0");
+  return WK_OK;
+}
+
+int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx** out) {
+  if (!out) { g_create_error = "out is NULL"; return WK_ERR_ARG; }
+  *out = nullptr;
+  wk_config c;
+  if (cfg) c = *cfg; else wk_config_defaults(&c);
+  if (n_env <= 0) { g_create_error = "n_env must be > 0"; return WK_ERR_ARG; }
+  std::string why;
+  int vs = validate(&c, why);
+  if (vs != WK_OK) { g_create_error = why; return vs; }
+  int ndev = 0;
+  hipError_t he = hipGetDeviceCount(&ndev);
+  if (he != hipSuccess || ndev == 0) {
+    g_create_error = std::string("no HIP device available: ") + hipGetErrorString(he);
+    return WK_ERR_HIP;
+  }
+  if (device < 0 || device >= ndev) { g_create_error = "device index out of range"; return WK_ERR_ARG; }
+  wk_ctx* x = new wk_ctx();
+  x->cfg = c;
+  x->cfg.CriticNeuralNetwork = nullptr;
+  x->cfg.ActorNeuralNetwork = nullptr;
+  if (x->cfg.Minibatch == 0) x->cfg.Minibatch = x->cfg.BatchSize;
+  x->device = device;
+  x->n = n_env;
+  x->seed = seed;
+  x->T = c.Horizon;
+  auto fail = [&](int code) {
+    g_create_error = x->err;
+    wk_destroy(x);
+    return code;
+  };
+  if (hipSetDevice(device) != hipSuccess) { x->err = "hipSetDevice failed"; return fail(WK_ERR_HIP); }
+  if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) {
+    x->err = "hipStreamCreate failed";
+    return fail(WK_ERR_HIP);
+  }
+  auto& P = x->P;
+  P.n_env = n_env;
+  P.iterations = c.Iterations;
+  P.max_timesteps = c.MaxTimesteps;
+  P.dt_frame = c.DeltaTime;
+  P.dt_sub = c.DeltaTime / (float)c.Iterations;
+  P.log_std = c.LogStandardDeviation;
+  P.std_ = expf(c.LogStandardDeviation);
+  P.seed = seed;
+  P.env_offset = c.EnvOffset;
+  const float PI_F = 3.14159265358979323846f;
+  x->lp_const = -logf(P.std_) - logf(sqrtf(2.0f * PI_F));
+
+  const size_t n = (size_t)n_env, T = (size_t)x->T;
+#define ALLOC(ptr, bytes)                                                   \
+  if (hipMalloc((void**)&(ptr), (bytes)) != hipSuccess) {                  \
+    x->err = "hipMalloc failed for " #ptr;                                  \
+    return fail(WK_ERR_HIP);                                                \
+  }
+  ALLOC(x->st, sizeof(float) * wk::NSTATE * n);
+  ALLOC(x->dxoff, sizeof(float) * n);
+  ALLOC(x->mat, sizeof(int32_t) * n);
+  ALLOC(x->rng_t, sizeof(uint32_t) * n);
+  ALLOC(x->W, sizeof(float) * wk::NPARAM);
+  ALLOC(x->m, sizeof(float) * wk::NPARAM);
+  ALLOC(x->v, sizeof(float) * wk::NPARAM);
+  ALLOC(x->grad, sizeof(float) * wk::SLAB);
+  ALLOC(x->ts, sizeof(float) * 12 * n * T);
+  ALLOC(x->ta, sizeof(float) * 4 * n * T);
+  ALLOC(x->tlp, sizeof(float) * 4 * n * T);
+  ALLOC(x->tr, sizeof(float) * n * T);
+  ALLOC(x->tv, sizeof(float) * n * T);
+  ALLOC(x->tret, sizeof(float) * n * T);
+  ALLOC(x->tadv, sizeof(float) * n * T);
+  ALLOC(x->td, n * T);
+#undef ALLOC
+  // synthetic randomisation of the initial state (BASELINE.json config 2 / 5)
+  std::vector<float> dx(n, 0.0f);
+  std::vector<int32_t> mt(n, WK_MAT_CARPET);
+  for (size_t e = 0; e < n; e++) {
+    uint32_t gid = (uint32_t)(c.EnvOffset + (int)e);
+    if (c.RandomizeStart) dx[e] = wk::env_offset(seed, gid);
+    if (c.RandomizeMaterial) mt[e] = wk::env_material(seed, gid);
+  }
+  if (hipMemcpy(x->dxoff, dx.data(), sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(x->mat, mt.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(x->rng_t, 0, sizeof(uint32_t) * n) != hipSuccess ||
+      hipMemset(x->m, 0, sizeof(float) * wk::NPARAM) != hipSuccess ||
+      hipMemset(x->v, 0, sizeof(float) * wk::NPARAM) != hipSuccess ||
+      hipMemset(x->td, 0, n * T) != hipSuccess) {
+    x->err = "initial upload failed";
+    return fail(WK_ERR_HIP);
+  }
+  if (wk::launch_env_init(P, x->st, x->dxoff, nullptr, 0, x->stream) != hipSuccess ||
+      wk::launch_xavier(x->W, seed, x->stream) != hipSuccess ||
+      hipStreamSynchronize(x->stream) != hipSuccess) {
+    x->err = "init kernels failed";
+    return fail(WK_ERR_HIP);
+  }
+  *out = x;
+  return WK_OK;
+}
+
+int wk_destroy(wk_ctx* c) {
+  if (!c) return WK_OK;
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (auto& e : c->pending) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
+  for (auto e : c->pool) hipEventDestroy(e);
+  if (c->comm) ncclCommDestroy(c->comm);
+  void* bufs[] = {c->st, c->dxoff, c->mat, c->rng_t, c->W, c->m, c->v, c->grad, c->ts, c->ta,
+                  c->tlp, c->tr, c->tv, c->tret, c->tadv, c->td, c->partial, c->scratch, c->scratch2};
+  for (void* p : bufs)
+    if (p) hipFree(p);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return WK_OK;
+}
+
+int wk_sync(wk_ctx* c) {
+  if (!c) return WK_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return WK_OK;
+}
+
+int wk_num_envs(const wk_ctx* c) { return c ? c->n : 0; }
+
+int wk_reset(wk_ctx* c, const uint8_t* mask) {
+  if (!c) return WK_ERR_ARG;
+  const uint8_t* dmask = nullptr;
+  if (mask) {
+    if (ensure(c, &c->scratch, &c->scratch_bytes, c->n)) return WK_ERR_HIP;
+    HIPCHK(c, hipMemcpyAsync(c->scratch, mask, c->n, hipMemcpyHostToDevice, c->stream));
+    dmask = (const uint8_t*)c->scratch;
+  }
+  // Environment.Reset re-creates the walker after the floor (post-reset body order)
+  HIPCHK(c, wk::launch_env_init(c->P, c->st, c->dxoff, dmask, 1, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return WK_OK;
+}
+
+int wk_set_materials(wk_ctx* c, const int32_t* mat_id) {
+  if (!c || !mat_id) return WK_ERR_ARG;
+  for (int e = 0; e < c->n; e++)
+    if (mat_id[e] < 0 || mat_id[e] > 7) { SETERR(c, "invalid material id %d at env %d", mat_id[e], e); return WK_ERR_ARG; }
+  HIPCHK(c, hipMemcpy(c->mat, mat_id, sizeof(int32_t) * c->n, hipMemcpyHostToDevice));
+  return WK_OK;
+}
+
+int wk_set_offsets(wk_ctx* c, const float* dx) {
+  if (!c || !dx) return WK_ERR_ARG;
+  HIPCHK(c, hipMemcpy(c->dxoff, dx, sizeof(float) * c->n, hipMemcpyHostToDevice));
+  return WK_OK;
+}
+
+static int step_impl(wk_ctx* c, const float* d_actions, int k, float* d_obs, float* d_rew,
+                     uint8_t* d_done, uint32_t* d_fault, int mode, void* trace) {
+  wk::StepArgs A{};
+  A.st = c->st; A.dxoff = c->dxoff; A.mat = c->mat; A.rng_t = c->rng_t;
+  A.actions = d_actions; A.obs_out = d_obs; A.rew_out = d_rew; A.done_out = d_done;
+  A.fault_out = d_fault; A.W = c->W; A.lp_const = c->lp_const;
+  A.traj_s = c->ts; A.traj_a = c->ta; A.traj_lp = c->tlp; A.traj_r = c->tr; A.traj_d = c->td;
+  A.traj_v = c->tv; A.t0 = 0;
+  A.trace = (wk::PairTraceDev*)trace;
+  A.k_steps = k;
+  ProfScope ps(c, PK_PHYS, (int64_t)k * c->n);
+  HIPCHK(c, wk::launch_env_step(mode, c->P, A, c->stream));
+  return WK_OK;
+}
+
+int wk_step_device(wk_ctx* c, const float* d_actions, int k, float* d_obs, float* d_rew,
+                   uint8_t* d_done, uint32_t* d_fault) {
+  if (!c || k <= 0) return WK_ERR_ARG;
+  return step_impl(c, d_actions, k, d_obs, d_rew, d_done, d_fault, d_actions ? 0 : 2, nullptr);
+}
+
+int wk_step(wk_ctx* c, const float* actions, int k, float* obs, float* reward, uint8_t* done,
+            uint32_t* fault) {
+  if (!c || k <= 0) return WK_ERR_ARG;
+  const size_t n = c->n;
+  const size_t b_act = actions ? sizeof(float) * 4 * n * k : 0;
+  const size_t b_obs = sizeof(float) * 12 * n * k, b_rew = sizeof(float) * n * k, b_done = n * k;
+  const size_t b_fault = sizeof(uint32_t) * n;
+  const size_t total = b_act + b_obs + b_rew + b_done + b_fault + 64;
+  if (ensure(c, &c->scratch2, &c->scratch2_bytes, total)) return WK_ERR_HIP;
+  char* base = (char*)c->scratch2;
+  float* d_act = actions ? (float*)base : nullptr;
+  float* d_obs = (float*)(base + b_act);
+  float* d_rew = (float*)(base + b_act + b_obs);
+  uint32_t* d_fault = (uint32_t*)(base + b_act + b_obs + b_rew);
+  uint8_t* d_done = (uint8_t*)(base + b_act + b_obs + b_rew + b_fault);
+  if (actions) HIPCHK(c, hipMemcpyAsync(d_act, actions, b_act, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(d_fault, 0, b_fault, c->stream));
+  int r = step_impl(c, d_act, k, obs ? d_obs : nullptr, reward ? d_rew : nullptr,
+                    done ? d_done : nullptr, d_fault, actions ? 0 : 2, nullptr);
+  if (r) return r;
+  if (obs) HIPCHK(c, hipMemcpyAsync(obs, d_obs, b_obs, hipMemcpyDeviceToHost, c->stream));
+  if (reward) HIPCHK(c, hipMemcpyAsync(reward, d_rew, b_rew, hipMemcpyDeviceToHost, c->stream));
+  if (done) HIPCHK(c, hipMemcpyAsync(done, d_done, b_done, hipMemcpyDeviceToHost, c->stream));
+  if (fault) HIPCHK(c, hipMemcpyAsync(fault, d_fault, b_fault, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return WK_OK;
+}
+
+int wk_step_traced(wk_ctx* c, const float* actions, wk_pair_trace* trace) {
+  if (!c || !actions || !trace) return WK_ERR_ARG;
+  static_assert(sizeof(wk_pair_trace) == 32 + 9 * 12, "trace layout");
+  const size_t n = c->n;
+  const size_t b_act = sizeof(float) * 4 * n;
+  const size_t b_tr = sizeof(wk_pair_trace) * n * c->cfg.Iterations;
+  if (ensure(c, &c->scratch2, &c->scratch2_bytes, b_act + b_tr + 64)) return WK_ERR_HIP;
+  float* d_act = (float*)c->scratch2;
+  void* d_tr = (char*)c->scratch2 + ((b_act + 63) / 64) * 64;
+  HIPCHK(c, hipMemcpyAsync(d_act, actions, b_act, hipMemcpyHostToDevice, c->stream));
+  int r = step_impl(c, d_act, 1, nullptr, nullptr, nullptr, nullptr, 1, d_tr);
+  if (r) return r;
+  HIPCHK(c, hipMemcpyAsync(trace, d_tr, b_tr, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return WK_OK;
+}
+
+int wk_get_obs(wk_ctx* c, float* obs) {
+  if (!c || !obs) return WK_ERR_ARG;
+  if (ensure(c, &c->scratch, &c->scratch_bytes, sizeof(float) * 12 * c->n)) return WK_ERR_HIP;
+  HIPCHK(c, wk::launch_get_obs(c->P, c->st, (float*)c->scratch, c->stream));
+  HIPCHK(c, hipMemcpyAsync(obs, c->scratch, sizeof(float) * 12 * c->n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return WK_OK;
+}
+
+int wk_get_state(wk_ctx* c, float* state) {
+  if (!c || !state) return WK_ERR_ARG;
+  std::vector<float> soa((size_t)wk::NSTATE * c->n);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(soa.data(), c->st, sizeof(float) * soa.size(), hipMemcpyDeviceToHost));
+  for (int e = 0; e < c->n; e++)
+    for (int f = 0; f < wk::NSTATE; f++) state[(size_t)e * wk::NSTATE + f] = soa[(size_t)f * c->n + e];
+  return WK_OK;
+}
+
+int wk_set_state(wk_ctx* c, const float* state) {
+  if (!c || !state) return WK_ERR_ARG;
+  std::vector<float> soa((size_t)wk::NSTATE * c->n);
+  for (int e = 0; e < c->n; e++)
+    for (int f = 0; f < wk::NSTATE; f++) soa[(size_t)f * c->n + e] = state[(size_t)e * wk::NSTATE + f];
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(c->st, soa.data(), sizeof(float) * soa.size(), hipMemcpyHostToDevice));
+  return WK_OK;
+}
+
+int wk_get_body_view(wk_ctx* c, int env, int body, wk_body_view* o) {
+  if (!c || !o || env < 0 || env >= c->n || body < 0 || body > 5) return WK_ERR_ARG;
+  memset(o, 0, sizeof(*o));
+  if (body == 5) {  // the static Metal floor (Environment.cs:219-223)
+    const float fl[4][2] = {{-50, 1050}, {-50, 900}, {1050, 900}, {1050, 1050}};
+    o->n_vertices = 4;
+    for (int i = 0; i < 4; i++) { o->vertices[i][0] = fl[i][0]; o->vertices[i][1] = fl[i][1]; }
+    o->centroid[0] = 500.0f; o->centroid[1] = 975.0f;
+    o->is_static = 1;
+    return WK_OK;
+  }
+  float f[wk::BSTRIDE];
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int i = 0; i < wk::BSTRIDE; i++)
+    HIPCHK(c, hipMemcpy(&f[i], c->st + (size_t)(body * wk::BSTRIDE + i) * c->n + env, sizeof(float), hipMemcpyDeviceToHost));
+  o->n_vertices = body == wk::BODY ? 5 : 6;
+  for (int i = 0; i < o->n_vertices; i++) { o->vertices[i][0] = f[2 * i]; o->vertices[i][1] = f[2 * i + 1]; }
+  o->centroid[0] = f[wk::F_CX]; o->centroid[1] = f[wk::F_CY];
+  o->linear_velocity[0] = f[wk::F_VX]; o->linear_velocity[1] = f[wk::F_VY];
+  o->angular_velocity = f[wk::F_W];
+  o->angle = f[wk::F_TH];
+  o->collided = f[wk::F_COL] != 0.0f;
+  return WK_OK;
+}
+
+int wk_get_weights(wk_ctx* c, float* p) {
+  if (!c || !p) return WK_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(p, c->W, sizeof(float) * wk::NPARAM, hipMemcpyDeviceToHost));
+  return WK_OK;
+}
+int wk_set_weights(wk_ctx* c, const float* p) {
+  if (!c || !p) return WK_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(c->W, p, sizeof(float) * wk::NPARAM, hipMemcpyHostToDevice));
+  return WK_OK;
+}
+int wk_get_adam(wk_ctx* c, float* m, float* v, int* t) {
+  if (!c) return WK_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (m) HIPCHK(c, hipMemcpy(m, c->m, sizeof(float) * wk::NPARAM, hipMemcpyDeviceToHost));
+  if (v) HIPCHK(c, hipMemcpy(v, c->v, sizeof(float) * wk::NPARAM, hipMemcpyDeviceToHost));
+  if (t) *t = c->adam_t;
+  return WK_OK;
+}
+int wk_set_adam(wk_ctx* c, const float* m, const float* v, int t) {
+  if (!c || t < 0) return WK_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (m) HIPCHK(c, hipMemcpy(c->m, m, sizeof(float) * wk::NPARAM, hipMemcpyHostToDevice));
+  if (v) HIPCHK(c, hipMemcpy(c->v, v, sizeof(float) * wk::NPARAM, hipMemcpyHostToDevice));
+  c->adam_t = t;
+  return WK_OK;
+}
+
+static int policy_impl(wk_ctx* c, int n, const float* obs, const int32_t* ids, const uint32_t* steps,
+                       float* mean, float* act, float* logp, float* v) {
+  const size_t b_obs = sizeof(float) * 12 * n, b4 = sizeof(float) * 4 * n, b1 = sizeof(float) * n;
+  const size_t total = b_obs + 3 * b4 + 2 * b1 + 2 * sizeof(int32_t) * n + 256;
+  if (ensure(c, &c->scratch2, &c->scratch2_bytes, total)) return WK_ERR_HIP;
+  char* p = (char*)c->scratch2;
+  float* d_obs = (float*)p; p += b_obs;
+  float* d_mean = (float*)p; p += b4;
+  float* d_act = (float*)p; p += b4;
+  float* d_lp = (float*)p; p += b4;
+  float* d_v = (float*)p; p += b1;
+  int32_t* d_ids = (int32_t*)p; p += sizeof(int32_t) * n;
+  uint32_t* d_steps = (uint32_t*)p;
+  HIPCHK(c, hipMemcpyAsync(d_obs, obs, b_obs, hipMemcpyHostToDevice, c->stream));
+  if (ids) HIPCHK(c, hipMemcpyAsync(d_ids, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+  if (steps) HIPCHK(c, hipMemcpyAsync(d_steps, steps, sizeof(uint32_t) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, wk::launch_policy(c->P, c->W, c->lp_const, n, d_obs, ids ? d_ids : nullptr,
+                              steps ? d_steps : nullptr, v ? nullptr : d_mean, v ? nullptr : d_act,
+                              v ? nullptr : d_lp, v ? d_v : nullptr, c->stream));
+  if (v) {
+    HIPCHK(c, hipMemcpyAsync(v, d_v, b1, hipMemcpyDeviceToHost, c->stream));
+  } else {
+    if (mean) HIPCHK(c, hipMemcpyAsync(mean, d_mean, b4, hipMemcpyDeviceToHost, c->stream));
+    if (act) HIPCHK(c, hipMemcpyAsync(act, d_act, b4, hipMemcpyDeviceToHost, c->stream));
+    if (logp) HIPCHK(c, hipMemcpyAsync(logp, d_lp, b4, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return WK_OK;
+}
+
+int wk_policy_sample(wk_ctx* c, int n, const float* obs, const int32_t* env_ids,
+                     const uint32_t* steps, float* mean, float* act, float* logp) {
+  if (!c || n <= 0 || !obs) return WK_ERR_ARG;
+  return policy_impl(c, n, obs, env_ids, steps, mean, act, logp, nullptr);
+}
+
+int wk_value(wk_ctx* c, int n, const float* obs, float* v) {
+  if (!c || n <= 0 || !obs || !v) return WK_ERR_ARG;
+  return policy_impl(c, n, obs, nullptr, nullptr, nullptr, nullptr, nullptr, v);
+}
+
+static int returns_impl(wk_ctx* c) {
+  {
+    ProfScope ps(c, PK_RET);
+    HIPCHK(c, wk::launch_returns(c->n, c->T_valid, c->cfg.UseGAE, c->cfg.Gamma, c->cfg.Lambda,
+                                 c->tr, c->tv, c->td, c->tret, c->tadv, c->stream));
+  }
+  if (c->cfg.NormalizeAdvantages)
+    HIPCHK(c, wk::launch_normalize(c->tadv, c->n * c->T_valid, c->cfg.Epsilon, c->stream));
+  c->returns_valid = true;
+  return WK_OK;
+}
+
+int wk_rollout(wk_ctx* c, int horizon) {
+  if (!c) return WK_ERR_ARG;
+  if (horizon <= 0) horizon = c->T;
+  if (horizon > c->T) { SETERR(c, "horizon %d exceeds the configured Horizon %d", horizon, c->T); return WK_ERR_ARG; }
+  wk::StepArgs A{};
+  A.st = c->st; A.dxoff = c->dxoff; A.mat = c->mat; A.rng_t = c->rng_t;
+  A.W = c->W; A.lp_const = c->lp_const;
+  A.traj_s = c->ts; A.traj_a = c->ta; A.traj_lp = c->tlp; A.traj_r = c->tr; A.traj_d = c->td;
+  A.traj_v = c->tv; A.t0 = 0; A.k_steps = horizon;
+  {
+    ProfScope ps(c, PK_PHYS, (int64_t)horizon * c->n);
+    HIPCHK(c, wk::launch_env_step(3, c->P, A, c->stream));
+  }
+  c->T_valid = horizon;
+  return returns_impl(c);
+}
+
+int wk_compute_returns(wk_ctx* c) {
+  if (!c) return WK_ERR_ARG;
+  if (c->T_valid <= 0) { SETERR(c, "no trajectory recorded"); return WK_ERR_STATE; }
+  return returns_impl(c);
+}
+
+int wk_rollout_stats_get(wk_ctx* c, wk_rollout_stats* o) {
+  if (!c || !o) return WK_ERR_ARG;
+  memset(o, 0, sizeof(*o));
+  const size_t cnt = (size_t)c->n * c->T_valid;
+  std::vector<float> r(cnt);
+  std::vector<uint8_t> d(cnt);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (cnt) {
+    HIPCHK(c, hipMemcpy(r.data(), c->tr, sizeof(float) * cnt, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(d.data(), c->td, cnt, hipMemcpyDeviceToHost));
+  }
+  for (size_t i = 0; i < cnt; i++) { o->reward_sum += r[i]; o->episodes += d[i]; }
+  o->env_steps = (int64_t)cnt;
+  return WK_OK;
+}
+
+int wk_get_trajectory(wk_ctx* c, float* s, float* a, float* lp, float* r, uint8_t* d, float* v,
+                      float* ret, float* adv) {
+  if (!c) return WK_ERR_ARG;
+  const size_t cnt = (size_t)c->n * c->T_valid;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (s) HIPCHK(c, hipMemcpy(s, c->ts, sizeof(float) * 12 * cnt, hipMemcpyDeviceToHost));
+  if (a) HIPCHK(c, hipMemcpy(a, c->ta, sizeof(float) * 4 * cnt, hipMemcpyDeviceToHost));
+  if (lp) HIPCHK(c, hipMemcpy(lp, c->tlp, sizeof(float) * 4 * cnt, hipMemcpyDeviceToHost));
+  if (r) HIPCHK(c, hipMemcpy(r, c->tr, sizeof(float) * cnt, hipMemcpyDeviceToHost));
+  if (d) HIPCHK(c, hipMemcpy(d, c->td, cnt, hipMemcpyDeviceToHost));
+  if (v) HIPCHK(c, hipMemcpy(v, c->tv, sizeof(float) * cnt, hipMemcpyDeviceToHost));
+  if (ret) HIPCHK(c, hipMemcpy(ret, c->tret, sizeof(float) * cnt, hipMemcpyDeviceToHost));
+  if (adv) HIPCHK(c, hipMemcpy(adv, c->tadv, sizeof(float) * cnt, hipMemcpyDeviceToHost));
+  return WK_OK;
+}
+
+int wk_set_trajectory(wk_ctx* c, int horizon, const float* s, const float* a, const float* lp,
+                      const float* r, const uint8_t* d, const float* v) {
+  if (!c || horizon <= 0 || horizon > c->T || !s || !a || !lp || !r || !d || !v) return WK_ERR_ARG;
+  const size_t cnt = (size_t)c->n * horizon;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(c->ts, s, sizeof(float) * 12 * cnt, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->ta, a, sizeof(float) * 4 * cnt, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->tlp, lp, sizeof(float) * 4 * cnt, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->tr, r, sizeof(float) * cnt, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->td, d, cnt, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->tv, v, sizeof(float) * cnt, hipMemcpyHostToDevice));
+  c->T_valid = horizon;
+  c->returns_valid = false;
+  return WK_OK;
+}
+
+// one minibatch: gradient kernel -> ordered block reduction -> [RCCL all-reduce] -> Adam
+static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
+  const int per_block = wpb * g.spw;
+  const int nblocks = (g.samples + per_block - 1) / per_block;
+  const size_t need = (size_t)nblocks * wk::SLAB;
+  if (c->partial_floats < need) {
+    if (c->partial) hipFree(c->partial);
+    c->partial = nullptr;
+    c->partial_floats = 0;
+    HIPCHK(c, hipMalloc((void**)&c->partial, sizeof(float) * need));
+    c->partial_floats = need;
+  }
+  g.partial = c->partial;
+  {
+    ProfScope ps(c, PK_GRAD);
+    HIPCHK(c, wk::launch_ppo_grad(g, wpb, nblocks, c->stream));
+  }
+  {
+    ProfScope ps(c, PK_REDUCE);
+    HIPCHK(c, wk::launch_grad_reduce(c->partial, nblocks, c->grad, c->stream));
+  }
+  if (c->comm && c->nranks > 1) {
+    ProfScope ps(c, PK_ALLRED);
+    ncclResult_t r = ncclAllReduce(c->grad, c->grad, wk::SLAB, ncclFloat, ncclSum,
+                                   c->comm, c->stream);
+    if (r != ncclSuccess) { SETERR(c, "ncclAllReduce: %s", ncclGetErrorString(r)); return WK_ERR_COMM; }
+  }
+  if (apply_adam) {
+    c->adam_t += 1;
+    const wk_config& k = c->cfg;
+    wk::AdamArgs a;
+    a.W = c->W; a.m = c->m; a.v = c->v; a.grad = c->grad;
+    a.c1 = 1.0f - k.Beta1;
+    a.c2 = 1.0f - k.Beta2;
+    a.beta1 = k.Beta1;
+    a.beta2 = k.Beta2;
+    a.bc1 = (float)(1.0 - pow((double)k.Beta1, (double)c->adam_t));
+    a.bc2 = (float)(1.0 - pow((double)k.Beta2, (double)c->adam_t));
+    a.alpha = k.Alpha;
+    a.eps = k.AdamEpsilon;
+    ProfScope ps(c, PK_ADAM);
+    HIPCHK(c, wk::launch_adam(a, c->stream));
+  }
+  return WK_OK;
+}
+
+static wk::GradArgs grad_base(wk_ctx* c) {
+  wk::GradArgs g{};
+  g.W = c->W;
+  g.std_ = c->P.std_;
+  g.lp_const = c->lp_const;
+  g.upper = 1.0f + c->cfg.Epsilon;
+  g.lower = 1.0f - c->cfg.Epsilon;
+  return g;
+}
+
+int wk_ppo_update(wk_ctx* c, const wk_ppo_args* args, float* critic_diag, float* actor_diag) {
+  if (!c) return WK_ERR_ARG;
+  if (c->T_valid <= 0) { SETERR(c, "wk_ppo_update before wk_rollout / wk_set_trajectory"); return WK_ERR_STATE; }
+  if (!c->returns_valid) {
+    int r = returns_impl(c);
+    if (r) return r;
+  }
+  const int epochs = (args && args->epochs > 0) ? args->epochs : c->cfg.Epochs;
+  const int M = (args && args->minibatch > 0) ? args->minibatch : c->cfg.Minibatch;
+  int Mg = (args && args->minibatch_global > 0) ? args->minibatch_global : c->cfg.MinibatchGlobal;
+  if (Mg <= 0) Mg = M * c->nranks;
+  const uint32_t update = args ? args->update_index : 0u;
+  const uint32_t pool = (uint32_t)((size_t)c->n * c->T_valid);
+  const int nmb = (int)(pool / (uint32_t)M);  // remainder dropped (PPOAgent.cs:506)
+  if (nmb <= 0) { SETERR(c, "minibatch %d larger than the pool %u", M, pool); return WK_ERR_ARG; }
+  const int wpb = 4;
+  int spw = (M + wpb * 256 - 1) / (wpb * 256);
+  if (spw < 1) spw = 1;
+  wk::GradArgs g = grad_base(c);
+  g.states = c->ts; g.actions = c->ta; g.logp_old = c->tlp; g.returns = c->tret; g.adv = c->tadv;
+  g.pool = pool;
+  g.use_perm = 1;
+  g.samples = M;
+  g.spw = spw;
+  g.b_div = (float)Mg;
+  for (int e = 0; e < epochs; e++) {
+    g.pk = wk::perm_key(c->seed, update, (uint32_t)e, pool);
+    for (int j = 0; j < nmb; j++) {
+      g.base = (uint32_t)j * (uint32_t)M;
+      int r = minibatch(c, g, wpb, 1);
+      if (r) return r;
+    }
+  }
+  float diag[3] = {0, 0, 0};
+  HIPCHK(c, hipMemcpyAsync(diag, c->grad + wk::NPARAM, sizeof(diag), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (critic_diag) *critic_diag = diag[0];
+  if (actor_diag) *actor_diag = diag[1];
+  return WK_OK;
+}
+
+int wk_train_batch(wk_ctx* c, int B, float b_div, const float* s, const float* a, const float* lpo,
+                   const float* ret, const float* adv, float* cd, float* ad, float* grads_out,
+                   int apply_adam, int* skipped) {
+  if (!c || B <= 0 || !s || !a || !lpo || !ret || !adv) return WK_ERR_ARG;
+  const size_t bs = sizeof(float) * B;
+  const size_t total = bs * (12 + 4 + 4 + 1 + 1) + 256;
+  if (ensure(c, &c->scratch2, &c->scratch2_bytes, total)) return WK_ERR_HIP;
+  char* p = (char*)c->scratch2;
+  float* d_s = (float*)p; p += bs * 12;
+  float* d_a = (float*)p; p += bs * 4;
+  float* d_l = (float*)p; p += bs * 4;
+  float* d_r = (float*)p; p += bs;
+  float* d_v = (float*)p;
+  HIPCHK(c, hipMemcpyAsync(d_s, s, bs * 12, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_a, a, bs * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_l, lpo, bs * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_r, ret, bs, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_v, adv, bs, hipMemcpyHostToDevice, c->stream));
+  wk::GradArgs g = grad_base(c);
+  g.states = d_s; g.actions = d_a; g.logp_old = d_l; g.returns = d_r; g.adv = d_v;
+  g.pool = (uint32_t)B;
+  g.base = 0;
+  g.use_perm = 0;
+  g.samples = B;
+  g.spw = B;  // one wave, samples in order: the reference's sequential accumulation
+  g.b_div = b_div;
+  int r = minibatch(c, g, 1, apply_adam);
+  if (r) return r;
+  std::vector<float> slab(wk::SLAB);
+  HIPCHK(c, hipMemcpyAsync(slab.data(), c->grad, sizeof(float) * slab.size(), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (grads_out) memcpy(grads_out, slab.data(), sizeof(float) * wk::NPARAM);
+  if (cd) *cd = slab[wk::NPARAM];
+  if (ad) *ad = slab[wk::NPARAM + 1];
+  if (skipped) *skipped = (int)slab[wk::NPARAM + 2];
+  return WK_OK;
+}
+
+int wk_comm_unique_id(uint8_t* id) {
+  if (!id) return WK_ERR_ARG;
+  static_assert(sizeof(ncclUniqueId) == 128, "nccl id size");
+  ncclUniqueId u;
+  ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) { g_create_error = ncclGetErrorString(r); return WK_ERR_COMM; }
+  memcpy(id, &u, sizeof(u));
+  return WK_OK;
+}
+
+int wk_comm_init(wk_ctx* c, int rank, int nranks, const uint8_t* id) {
+  if (!c || !id || nranks <= 0 || rank < 0 || rank >= nranks) return WK_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess) { SETERR(c, "ncclCommInitRank: %s", ncclGetErrorString(r)); c->comm = nullptr; return WK_ERR_COMM; }
+  c->rank = rank;
+  c->nranks = nranks;
+  return WK_OK;
+}
+
+int wk_allreduce_test(wk_ctx* c, float* host_buf, int n) {
+  if (!c || !host_buf || n <= 0) return WK_ERR_ARG;
+  if (ensure(c, &c->scratch, &c->scratch_bytes, sizeof(float) * n)) return WK_ERR_HIP;
+  HIPCHK(c, hipMemcpyAsync(c->scratch, host_buf, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  if (c->comm && c->nranks > 1) {
+    ncclResult_t r = ncclAllReduce(c->scratch, c->scratch, n, ncclFloat, ncclSum, c->comm, c->stream);
+    if (r != ncclSuccess) { SETERR(c, "ncclAllReduce: %s", ncclGetErrorString(r)); return WK_ERR_COMM; }
+  }
+  HIPCHK(c, hipMemcpyAsync(host_buf, c->scratch, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return WK_OK;
+}
+
+int wk_profile_enable(wk_ctx* c, int on) {
+  if (!c) return WK_ERR_ARG;
+  c->prof = on != 0;
+  return WK_OK;
+}
+
+int wk_profile_reset(wk_ctx* c) {
+  if (!c) return WK_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  prof_drain(c);
+  for (int i = 0; i < PK_N; i++) { c->prof_ms[i] = 0; c->prof_cnt[i] = 0; }
+  c->prof_units = 0;
+  return WK_OK;
+}
+
+int wk_profile_get(wk_ctx* c, wk_profile* o) {
+  if (!c || !o) return WK_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  prof_drain(c);
+  o->physics_ms = c->prof_ms[PK_PHYS]; o->physics_launches = c->prof_cnt[PK_PHYS];
+  o->physics_env_steps = c->prof_units;
+  o->grad_ms = c->prof_ms[PK_GRAD]; o->grad_launches = c->prof_cnt[PK_GRAD];
+  o->reduce_ms = c->prof_ms[PK_REDUCE]; o->reduce_launches = c->prof_cnt[PK_REDUCE];
+  o->adam_ms = c->prof_ms[PK_ADAM]; o->adam_launches = c->prof_cnt[PK_ADAM];
+  o->allreduce_ms = c->prof_ms[PK_ALLRED]; o->allreduce_calls = c->prof_cnt[PK_ALLRED];
+  o->returns_ms = c->prof_ms[PK_RET]; o->returns_launches = c->prof_cnt[PK_RET];
+  return WK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+// wk_kernels.h -- kernel argument blocks and host launch shims shared by
+// wk_physics.hip, wk_ppo.hip and wk_api.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "wk_common.h"
+
+namespace wk {
+
+// per-substep pair bookkeeping; layout == wk_pair_trace (include/wk_api.h)
+struct PairTraceDev {
+  uint8_t aabb_hit[9];
+  uint8_t sat_hit[9];
+  uint8_t n_contacts[9];
+  uint8_t pad[5];
+  float normal[9][2];
+  float depth[9];
+};
+
+struct StepArgs {
+  float* st;                 // SoA state [NSTATE][n]
+  const float* dxoff;        // [n] start offset (x = 125 + dx)
+  const int32_t* mat;        // [n] material id
+  uint32_t* rng_t;           // [n] per-env env-step counter (Philox counter)
+  const float* actions;      // [k][n][4] or null (policy)
+  float* obs_out;            // [k][n][12] or null
+  float* rew_out;            // [k][n] or null
+  uint8_t* done_out;         // [k][n] or null
+  uint32_t* fault_out;       // [n] or null (OR-accumulated)
+  const float* W;            // params (policy)
+  float lp_const;            // -ln(std) - ln(sqrt(2 pi))
+  // trajectory buffer (RECORD), index t*n + e
+  float* traj_s; float* traj_a; float* traj_lp; float* traj_r; uint8_t* traj_d; float* traj_v;
+  int t0;
+  PairTraceDev* trace;       // [n][iterations] (TRACE)
+  int k_steps;
+};
+
+struct GradArgs {
+  const float* W;        // params
+  const float* states;   // [P][12]
+  const float* actions;  // [P][4]
+  const float* logp_old; // [P][4]
+  const float* returns;  // [P]
+  const float* adv;      // [P]
+  uint32_t pool;         // P
+  uint32_t base;         // first permuted position of this minibatch
+  int use_perm;
+  PermKey pk;
+  int samples;           // samples in this minibatch (local)
+  int spw;               // samples per wave
+  float b_div;           // divisor of dV / dmu (BatchSize / global minibatch)
+  float std_;            // MathF.Exp(LogStandardDeviation)
+  float lp_const;        // -ln(std) - ln(sqrt(2 pi))
+  float upper, lower;    // 1 + eps, 1 - eps
+  float* partial;        // [nblocks][SLAB]
+};
+
+struct AdamArgs {
+  float* W; float* m; float* v; const float* grad;
+  float c1, c2, beta1, beta2, bc1, bc2, alpha, eps;
+};
+
+enum : int { SLAB = NPARAM + 4 };  // gradient + critic diag, actor diag, skipped, pad
+
+hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s);
+hipError_t launch_env_init(const EnvParams& P, float* st, const float* dx, const uint8_t* mask,
+                           int post, hipStream_t s);
+hipError_t launch_get_obs(const EnvParams& P, const float* st, float* obs, hipStream_t s);
+hipError_t launch_policy(const EnvParams& P, const float* W, float lp_const, int n,
+                         const float* obs, const int32_t* env_ids, const uint32_t* steps,
+                         float* mean, float* act, float* logp, float* v, hipStream_t s);
+hipError_t launch_returns(int n, int T, int use_gae, float gamma, float lambda, const float* r,
+                          const float* v, const uint8_t* d, float* ret, float* adv, hipStream_t s);
+hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t s);
+hipError_t launch_grad_reduce(const float* partial, int nblocks, float* grad, hipStream_t s);
+hipError_t launch_adam(const AdamArgs& a, hipStream_t s);
+hipError_t launch_normalize(float* x, int n, float eps, hipStream_t s);
+hipError_t launch_xavier(float* W, uint64_t seed, hipStream_t s);
+
+}  // namespace wk

@@ -1,0 +1,585 @@
+// wk_physics.hip -- fused batched env-step kernel for gfx950 (one walker per lane).
+//
+// One launch runs K whole Environment.Update steps (Environment.cs:64-92) for every
+// walker: optional policy sampling (PPOAgent.SampleActions, PPOAgent.cs:381-398),
+// Clip + Joint.SetTorque (Environment.cs:78, Joint.cs:56-61), Iterations substeps of
+// StepObjects (Environment.cs:126-143: Joint.Step Joint.cs:31-41, RigidBody.Step
+// Bodies/RigidBody.cs:54-61 with the AABB broadphase Skeleton.cs:133-140, SAT
+// Bodies/Physics/SATCollision.cs:15-104, contact clipping ContactPoints.cs:13-134 and
+// impulses Impulses.cs:12-115), Walker.Update (Walker.cs:49-54), CalculateReward
+// (Environment.cs:148-154), terminal checks (:106-117), GetState (Walker.cs:132-152)
+// and auto-reset (Environment.cs:167-180, Walker.cs:212-223).
+//
+// All walker state lives in VGPRs for the whole launch; HBM is touched only to load
+// and store the 112-float SoA state once per launch and to write per-step outputs.
+// Arithmetic is restated op-for-op in IEEE fp32 with -ffp-contract=off so the
+// trajectories are bit-identical to the CPU oracle (MonoGame Vector2 semantics:
+// v / f == v * (1/f); rotation via (float)cos/sin of the double-promoted angle).
+#include "wk_common.h"
+#include "wk_device.h"
+#include "wk_kernels.h"
+
+namespace wk {
+
+struct EnvState {
+  Poly<6> lll, llu, rll, rlu;
+  Poly<5> body;
+  Dyn dlll, dllu, dbody, drll, drlu;
+  bool clll, cllu, cbody, crll, crlu;
+  float torque[4];
+  float posx, posy, prevx, prevy;
+  int steps, episodes;
+  bool post, terminal;
+};
+
+// Pole.FromSize (Objects/RigidBodies/Pole.cs:18-34) + FindCentroid (Skeleton.cs:100-113)
+DEV void make_pole(Poly<6>& p, float cx, float cy) {
+  float adjustment = 0.1f * 75.0f;
+  float h = adjustment * 3.5f;
+  p.x[0] = cx + adjustment; p.y[0] = cy + h;
+  p.x[1] = cx;              p.y[1] = cy + h;
+  p.x[2] = cx - adjustment; p.y[2] = cy + h;
+  p.x[3] = cx - adjustment; p.y[3] = cy - h;
+  p.x[4] = cx;              p.y[4] = cy - h;
+  p.x[5] = cx + adjustment; p.y[5] = cy - h;
+  find_centroid(p);
+}
+
+DEV void zero_dyn(Dyn& d) { d.vx = 0.0f; d.vy = 0.0f; d.w = 0.0f; d.th = 0.0f; }
+
+// Walker.CreateCreature / Reset + Environment.InitialState
+DEV void make_template(EnvState& s, float dx) {
+  float px = 125.0f + dx, py = 800.0f;
+  s.body.x[0] = px + 20; s.body.y[0] = py + 20;
+  s.body.x[1] = px;      s.body.y[1] = py + 20;
+  s.body.x[2] = px - 20; s.body.y[2] = py + 20;
+  s.body.x[3] = px - 20; s.body.y[3] = py - 20;
+  s.body.x[4] = px + 20; s.body.y[4] = py - 20;
+  find_centroid(s.body);
+  make_pole(s.llu, px + 0.0f, py + 30.0f);
+  make_pole(s.lll, px + 0.0f, py + 60.0f);
+  make_pole(s.rlu, px + 0.0f, py + 30.0f);
+  make_pole(s.rll, px + 0.0f, py + 60.0f);
+  zero_dyn(s.dlll); zero_dyn(s.dllu); zero_dyn(s.dbody); zero_dyn(s.drll); zero_dyn(s.drlu);
+  s.clll = s.cllu = s.cbody = s.crll = s.crlu = false;
+#pragma unroll
+  for (int j = 0; j < 4; j++) s.torque[j] = 0.0f;
+  s.steps = 0;
+  s.terminal = false;
+  // InitialState -> Walker.Update: prev = (125, 800); pos = Body centroid
+  s.prevx = px; s.prevy = py;
+  s.posx = s.body.cx; s.posy = s.body.cy;
+}
+
+template <int N>
+DEV void load_poly(Poly<N>& p, const float* __restrict__ st, int b, int e, int n) {
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    p.x[i] = st[(b * BSTRIDE + 2 * i) * n + e];
+    p.y[i] = st[(b * BSTRIDE + 2 * i + 1) * n + e];
+  }
+  p.cx = st[(b * BSTRIDE + F_CX) * n + e];
+  p.cy = st[(b * BSTRIDE + F_CY) * n + e];
+}
+DEV void load_dyn(Dyn& d, bool& col, const float* __restrict__ st, int b, int e, int n) {
+  d.vx = st[(b * BSTRIDE + F_VX) * n + e];
+  d.vy = st[(b * BSTRIDE + F_VY) * n + e];
+  d.w = st[(b * BSTRIDE + F_W) * n + e];
+  d.th = st[(b * BSTRIDE + F_TH) * n + e];
+  col = st[(b * BSTRIDE + F_COL) * n + e] != 0.0f;
+}
+template <int N>
+DEV void store_body(const Poly<N>& p, const Dyn& d, bool col, float* __restrict__ st, int b, int e,
+                    int n) {
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    st[(b * BSTRIDE + 2 * i) * n + e] = i < N ? p.x[i < N ? i : 0] : 0.0f;
+    st[(b * BSTRIDE + 2 * i + 1) * n + e] = i < N ? p.y[i < N ? i : 0] : 0.0f;
+  }
+  st[(b * BSTRIDE + F_CX) * n + e] = p.cx;
+  st[(b * BSTRIDE + F_CY) * n + e] = p.cy;
+  st[(b * BSTRIDE + F_VX) * n + e] = d.vx;
+  st[(b * BSTRIDE + F_VY) * n + e] = d.vy;
+  st[(b * BSTRIDE + F_W) * n + e] = d.w;
+  st[(b * BSTRIDE + F_TH) * n + e] = d.th;
+  st[(b * BSTRIDE + F_COL) * n + e] = col ? 1.0f : 0.0f;
+  st[(b * BSTRIDE + 19) * n + e] = 0.0f;
+}
+
+DEV void load_state(EnvState& s, const float* __restrict__ st, int e, int n) {
+  load_poly(s.lll, st, LLL, e, n);
+  load_poly(s.llu, st, LLU, e, n);
+  load_poly(s.body, st, BODY, e, n);
+  load_poly(s.rll, st, RLL, e, n);
+  load_poly(s.rlu, st, RLU, e, n);
+  load_dyn(s.dlll, s.clll, st, LLL, e, n);
+  load_dyn(s.dllu, s.cllu, st, LLU, e, n);
+  load_dyn(s.dbody, s.cbody, st, BODY, e, n);
+  load_dyn(s.drll, s.crll, st, RLL, e, n);
+  load_dyn(s.drlu, s.crlu, st, RLU, e, n);
+#pragma unroll
+  for (int j = 0; j < 4; j++) s.torque[j] = st[(S_TORQUE + j) * n + e];
+  s.posx = st[S_POS * n + e];
+  s.posy = st[(S_POS + 1) * n + e];
+  s.prevx = st[S_PREV * n + e];
+  s.prevy = st[(S_PREV + 1) * n + e];
+  s.steps = (int)st[S_STEPS * n + e];
+  s.post = st[S_POSTRESET * n + e] != 0.0f;
+  s.terminal = st[S_TERMINAL * n + e] != 0.0f;
+  s.episodes = (int)st[S_EPISODES * n + e];
+}
+
+DEV void store_state(const EnvState& s, float* __restrict__ st, int e, int n) {
+  store_body(s.lll, s.dlll, s.clll, st, LLL, e, n);
+  store_body(s.llu, s.dllu, s.cllu, st, LLU, e, n);
+  store_body(s.body, s.dbody, s.cbody, st, BODY, e, n);
+  store_body(s.rll, s.drll, s.crll, st, RLL, e, n);
+  store_body(s.rlu, s.drlu, s.crlu, st, RLU, e, n);
+#pragma unroll
+  for (int j = 0; j < 4; j++) st[(S_TORQUE + j) * n + e] = s.torque[j];
+  st[S_POS * n + e] = s.posx;
+  st[(S_POS + 1) * n + e] = s.posy;
+  st[S_PREV * n + e] = s.prevx;
+  st[(S_PREV + 1) * n + e] = s.prevy;
+  st[S_STEPS * n + e] = (float)s.steps;
+  st[S_POSTRESET * n + e] = s.post ? 1.0f : 0.0f;
+  st[S_TERMINAL * n + e] = s.terminal ? 1.0f : 0.0f;
+  st[S_EPISODES * n + e] = (float)s.episodes;
+}
+
+// Walker.GetState (Walker.cs:132-152)
+DEV void get_obs(const EnvState& s, float o[12]) {
+  o[0] = s.body.x[1] / 900.0f;
+  o[1] = s.body.y[1] / 500.0f;
+  o[2] = s.llu.x[2] / 900.0f;
+  o[3] = s.llu.y[2] / 500.0f;
+  o[4] = s.rlu.x[2] / 900.0f;
+  o[5] = s.rlu.y[2] / 500.0f;
+  o[6] = s.dbody.vx / 60.0f;
+  o[7] = s.dbody.vy / 60.0f;
+  o[8] = s.dlll.th;
+  o[9] = s.dllu.th;
+  o[10] = s.drll.th;
+  o[11] = s.drlu.th;
+}
+
+// RigidBody.ResolveCollisions body for one (this=A, other=B) candidate
+// (Bodies/RigidBody.cs:66-96); B may be the static floor.
+template <int NA, int NB, bool BSTATIC, bool TRACE>
+DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB,
+                      bool& colA, PairTraceDev* tr, int pi) {
+  if (!aabb_overlap(A, B)) return;
+  if (TRACE) tr->aabb_hit[pi] = 1;
+  if (BSTATIC) colA = true;  // body._isFloor -> Collided = true (:75)
+  V2 n;
+  float depth;
+  if (!sat(A, B, n, depth)) return;
+  V2 c0, c1;
+  int nc = contact_points(A, B, n, c0, c1);
+  if (TRACE) {
+    tr->sat_hit[pi] = 1;
+    tr->n_contacts[pi] = (uint8_t)nc;
+    tr->normal[pi][0] = n.x;
+    tr->normal[pi][1] = n.y;
+    tr->depth[pi] = depth;
+  }
+  // MoveObjects (:99-113): A is never static here
+  if (BSTATIC) {
+    move(A, vmul(n, depth));
+  } else {
+    move(A, vdiv(vmul(n, depth), 2.0f));
+    move(B, vdiv(vmul(vneg(n), depth), 2.0f));
+  }
+  // Impulses.ResolveCollisions (Impulses.cs:12-28)
+  if (nc == 0) return;
+  float e = net_maxf(mA.e, mB.e);
+  float mu = net_minf(mA.mu, mB.mu);
+  V2 contact = nc == 2 ? vdiv(vadd(c0, c1), 2.0f) : c0;
+  Body bA{A.cx, A.cy, &dA, mA.im, mA.ii};
+  Body bB{B.cx, B.cy, &dB, mB.im, mB.ii};
+  V2 rA, rB, rAF, rBF;
+  float j = calc_impulse(bA, bB, contact, 1.0f + e, n, rA, rB);
+  V2 tangent = mk(-n.y, n.x);
+  float jf = calc_impulse(bA, bB, contact, mu, tangent, rAF, rBF);
+  apply_impulses<BSTATIC>(bA, bB, n, j, rA, rB);
+  apply_impulses<BSTATIC>(bA, bB, tangent, jf, rAF, rBF);
+}
+
+// Joint.Step (Objects/RigidBodies/Joint.cs:31-41); ResolveJoint swaps the bodies (:40)
+template <int NA, int NB, int IA, int IB>
+DEV void joint_step(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB) {
+  V2 ab = vsub(mk(B.x[IB], B.y[IB]), mk(A.x[IA], A.y[IA]));
+  float depth = vlen(ab);
+  if (depth < 0.1f) return;
+  ab = vnormalize(ab);
+  move(A, vdiv(vmul(ab, depth), 2.0f));
+  move(B, vdiv(vmul(vneg(ab), depth), 2.0f));
+  V2 contact = vdiv(vadd(mk(A.x[IA], A.y[IA]), mk(B.x[IB], B.y[IB])), 2.0f);
+  Body bJ{B.cx, B.cy, &dB, mB.im, mB.ii};  // manifold.BodyA = joint body B
+  Body bI{A.cx, A.cy, &dA, mA.im, mA.ii};  // manifold.BodyB = joint body A
+  V2 rA, rB;
+  float j = calc_impulse(bJ, bI, contact, 1.0f + 1.0f, ab, rA, rB);
+  apply_impulses<false>(bJ, bI, ab, j, rA, rB);
+}
+
+// RigidBody.StepLinearVelocity + StepAngularVelocity (RigidBody.cs:116-140)
+template <int N>
+DEV void integrate(Poly<N>& P, Dyn& D, float dt, float adx, float ady) {
+  D.vx = D.vx + adx;
+  D.vy = D.vy + ady;
+  move(P, mk(D.vx * dt, D.vy * dt));
+  D.th = D.th + D.w * dt;
+  D.th = wrap_angle(D.th);
+  rotate(P, D.w * dt);
+}
+
+// one substep of Environment.StepObjects (:130-142)
+template <bool TRACE>
+DEV void substep(EnvState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
+                 PairTraceDev* tr) {
+  Poly<4> fl;
+  floor_poly(fl);
+  Dyn dfl;
+  zero_dyn(dfl);
+  const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};  // Metal, static: inverse mass/inertia 0
+  // joints: [bodyJointLeft, bodyJointRight, leftJoint, rightJoint] (Walker.cs:182-187)
+  joint_step<5, 6, 1, 4>(s.body, s.dbody, mb, s.llu, s.dllu, mp);
+  joint_step<5, 6, 1, 4>(s.body, s.dbody, mb, s.rlu, s.drlu, mp);
+  joint_step<6, 6, 2, 3>(s.llu, s.dllu, mp, s.lll, s.dlll, mp);
+  joint_step<6, 6, 2, 3>(s.rlu, s.drlu, mp, s.rll, s.drll, mp);
+  // bodies in list order; the floor's own step is a no-op (static, zero velocity).
+  // Episode 0 lists the floor last, every later episode first (Walker.cs:212-234):
+  // that only changes the order of each leg segment's two candidate pairs.
+  integrate(s.lll, s.dlll, dt, adx, ady);
+#pragma unroll 1
+  for (int q = 0; q < 2; q++) {
+    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE>(s.lll, s.dlll, mp, fl, dfl, mf, s.clll, tr, 1);
+    else resolve_pair<6, 6, false, TRACE>(s.lll, s.dlll, mp, s.llu, s.dllu, mp, s.clll, tr, 0);
+  }
+  integrate(s.llu, s.dllu, dt, adx, ady);
+#pragma unroll 1
+  for (int q = 0; q < 2; q++) {
+    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE>(s.llu, s.dllu, mp, fl, dfl, mf, s.cllu, tr, 3);
+    else resolve_pair<6, 6, false, TRACE>(s.llu, s.dllu, mp, s.lll, s.dlll, mp, s.cllu, tr, 2);
+  }
+  integrate(s.body, s.dbody, dt, adx, ady);
+  resolve_pair<5, 4, true, TRACE>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody, tr, 4);
+  integrate(s.rll, s.drll, dt, adx, ady);
+#pragma unroll 1
+  for (int q = 0; q < 2; q++) {
+    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE>(s.rll, s.drll, mp, fl, dfl, mf, s.crll, tr, 6);
+    else resolve_pair<6, 6, false, TRACE>(s.rll, s.drll, mp, s.rlu, s.drlu, mp, s.crll, tr, 5);
+  }
+  integrate(s.rlu, s.drlu, dt, adx, ady);
+#pragma unroll 1
+  for (int q = 0; q < 2; q++) {
+    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE>(s.rlu, s.drlu, mp, fl, dfl, mf, s.crlu, tr, 8);
+    else resolve_pair<6, 6, false, TRACE>(s.rlu, s.drlu, mp, s.rll, s.drll, mp, s.crlu, tr, 7);
+  }
+}
+
+// ---------------- policy (fused, weights read with wave-uniform scalar loads) ----------
+// DenseLayer.FeedForward (DenseLayer.cs:82-98): z_j = (sum_k W[j][k] x[k], in order) + b_j
+DEV void actor_mean(const float* __restrict__ W, const float s[12], float mean[4]) {
+  float h1[64];
+#pragma unroll
+  for (int j = 0; j < 64; j++) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 12; k++) acc = acc + W[OFF_A_W1 + j * 12 + k] * s[k];
+    float z = acc + W[OFF_A_B1 + j];
+    h1[j] = net_maxf(0.2f * z, z);
+  }
+  float z3[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 2
+  for (int j = 0; j < 64; j++) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 64; k++) acc = acc + W[OFF_A_W2 + j * 64 + k] * h1[k];
+    float z = acc + W[OFF_A_B2 + j];
+    float h2 = net_maxf(0.2f * z, z);
+#pragma unroll
+    for (int d = 0; d < 4; d++) z3[d] = z3[d] + W[OFF_A_W3 + d * 64 + j] * h2;
+  }
+#pragma unroll
+  for (int d = 0; d < 4; d++) mean[d] = tanhf(z3[d] + W[OFF_A_B3 + d]);
+}
+
+DEV float critic_value(const float* __restrict__ W, const float s[12]) {
+  float v = 0.0f;
+#pragma unroll 4
+  for (int j = 0; j < 64; j++) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 12; k++) acc = acc + W[OFF_C_W1 + j * 12 + k] * s[k];
+    float z = acc + W[OFF_C_B1 + j];
+    float h = net_maxf(0.2f * z, z);
+    v = v + W[OFF_C_W2 + j] * h;
+  }
+  return v + W[OFF_C_B2];
+}
+
+// NormalDistribution.BoxMullerTransform (NormalDistribution.cs:12-19) with Philox draws
+DEV void sample_actions(const EnvParams& P, float lp_const, uint32_t gid, uint32_t t,
+                        const float mean[4], float act[4], float logp[4]) {
+  const float PI_F = 3.14159265358979323846f;
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    U4 o = philox(P.seed, gid, t, (uint32_t)d, ST_ACT);
+    float u1 = next_double_f(o.x, o.y);
+    float u2 = next_double_f(o.z, o.w);
+    if (u1 == 0.0f) u1 = 1.0f;
+    float z = sqrtf(-2.0f * logf(u1)) * sinf(2.0f * PI_F * u2);
+    act[d] = mean[d] + (P.std_ * z);
+  }
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    // LogProbabilityDensity (:24-32); lp_const = -ln(std) - ln(sqrt(2 pi)) (host libm)
+    float fraction = (act[d] - mean[d]) / P.std_;
+    fraction *= fraction;
+    fraction /= 2.0f;
+    logp[d] = lp_const - fraction;
+  }
+}
+
+DEV bool state_finite(const EnvState& s) {
+  float acc = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 6; i++) acc += s.lll.x[i] * 0.0f + s.llu.x[i] * 0.0f + s.rll.x[i] * 0.0f + s.rlu.x[i] * 0.0f;
+  acc += s.dbody.vx * 0.0f + s.dbody.vy * 0.0f + s.body.cx * 0.0f + s.body.cy * 0.0f;
+  return acc == 0.0f;
+}
+
+template <bool POLICY, bool RECORD, bool TRACE>
+__global__ __launch_bounds__(64) void k_env_step(EnvParams P, StepArgs A) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = P.n_env;
+  if (e >= n) return;
+  EnvState s;
+  load_state(s, A.st, e, n);
+  const float dx = A.dxoff[e];
+  const MatConst mc = material(A.mat[e]);
+  const Mat mp{mc.inv_mass, 0.001f * mc.inv_mass, mc.restitution, mc.friction};
+  const Mat mb{mc.inv_mass, 0.0003f, mc.restitution, mc.friction};  // Walker.cs:168
+  const float dt = P.dt_sub;
+  const float adx = 0.0f * dt, ady = 980.0f * dt;  // _acceleration * deltaTime
+  const uint32_t gid = (uint32_t)(P.env_offset + e);
+  uint32_t t = A.rng_t[e];
+  uint32_t fault = 0;
+
+#pragma unroll 1
+  for (int k = 0; k < A.k_steps; k++) {
+    float a[4], lp[4], obs[12];
+    if (POLICY) {
+      get_obs(s, obs);
+      float mean[4];
+      actor_mean(A.W, obs, mean);
+      sample_actions(P, A.lp_const, gid, t, mean, a, lp);
+      if (RECORD) {
+        const size_t idx = (size_t)(A.t0 + k) * n + e;
+        float v = critic_value(A.W, obs);
+#pragma unroll
+        for (int i = 0; i < 12; i++) A.traj_s[idx * 12 + i] = obs[i];
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+          A.traj_a[idx * 4 + d] = a[d];
+          A.traj_lp[idx * 4 + d] = lp[d];
+        }
+        A.traj_v[idx] = v;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < 4; d++) a[d] = A.actions[((size_t)k * n + e) * 4 + d];
+    }
+    // Environment.Update (:71-78)
+    s.steps++;
+    float ac[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) ac[d] = clip1(a[d]);
+    // Joint.SetTorque on joints [Body-LLU, Body-RLU, LLU-LLL, RLU-RLL]: child w += 5*change
+    {
+      float c;
+      c = ac[0] - s.torque[0]; s.torque[0] = ac[0]; s.dllu.w = s.dllu.w + c * 5.0f;
+      c = ac[1] - s.torque[1]; s.torque[1] = ac[1]; s.drlu.w = s.drlu.w + c * 5.0f;
+      c = ac[2] - s.torque[2]; s.torque[2] = ac[2]; s.dlll.w = s.dlll.w + c * 5.0f;
+      c = ac[3] - s.torque[3]; s.torque[3] = ac[3]; s.drll.w = s.drll.w + c * 5.0f;
+    }
+    // StepObjects
+#pragma unroll 1
+    for (int it = 0; it < P.iterations; it++) {
+      PairTraceDev* tr = nullptr;
+      if (TRACE) {
+        tr = A.trace + ((size_t)e * P.iterations + it);
+        PairTraceDev z = {};
+        *tr = z;
+      }
+      substep<TRACE>(s, mp, mb, dt, adx, ady, tr);
+    }
+    // Walker.Update
+    s.prevx = s.posx; s.prevy = s.posy;
+    s.posx = s.body.cx; s.posy = s.body.cy;
+    if (s.cbody || s.cllu || s.crlu) s.terminal = true;
+    // CalculateReward
+    float reward = 0.0f;
+    float dX = s.posx - s.prevx;
+    float yb = s.body.y[1];
+    reward = reward + ((dX > 0.0f && ((yb / 500.0f) < 1.6f)) ? dX : 0.0f);
+    reward = reward - (((yb / 500.0f) > 1.65f) ? -0.1f : 0.0f);
+    bool terminal = false;
+    if (s.terminal || s.steps > P.max_timesteps) {
+      if (s.terminal) reward -= 40.0f;
+      terminal = true;
+    }
+    if (s.posx > 900.0f) {
+      reward += 80.0f;
+      terminal = true;
+    }
+    if (!state_finite(s)) fault |= 1u;
+    if (terminal) {
+      int ep = s.episodes + 1;
+      make_template(s, dx);
+      s.post = true;
+      s.episodes = ep;
+    }
+    if (A.obs_out) {
+      get_obs(s, obs);
+#pragma unroll
+      for (int i = 0; i < 12; i++) A.obs_out[((size_t)k * n + e) * 12 + i] = obs[i];
+    }
+    if (A.rew_out) A.rew_out[(size_t)k * n + e] = reward;
+    if (A.done_out) A.done_out[(size_t)k * n + e] = terminal ? 1 : 0;
+    if (RECORD) {
+      const size_t idx = (size_t)(A.t0 + k) * n + e;
+      A.traj_r[idx] = reward;
+      A.traj_d[idx] = terminal ? 1 : 0;
+    }
+    t++;
+  }
+  store_state(s, A.st, e, n);
+  A.rng_t[e] = t;
+  if (A.fault_out) A.fault_out[e] |= fault;
+}
+
+// env initialisation: Environment ctor (Environment.cs:39-51) -- episode-0 body order
+__global__ void k_env_init(EnvParams P, float* st, const float* dxoff, const uint8_t* mask,
+                           int post) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.n_env) return;
+  if (mask && !mask[e]) return;
+  EnvState s;
+  int episodes = post ? (int)st[S_EPISODES * P.n_env + e] : 0;
+  make_template(s, dxoff[e]);
+  s.post = post != 0;
+  s.episodes = episodes;
+  store_state(s, st, e, P.n_env);
+}
+
+__global__ void k_get_obs(EnvParams P, const float* st, float* obs) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.n_env) return;
+  EnvState s;
+  load_state(s, st, e, P.n_env);
+  float o[12];
+  get_obs(s, o);
+  for (int i = 0; i < 12; i++) obs[(size_t)e * 12 + i] = o[i];
+}
+
+// standalone policy evaluation (wk_policy_sample / wk_value)
+__global__ void k_policy(EnvParams P, const float* __restrict__ W, float lp_const, int n,
+                         const float* obs, const int32_t* env_ids, const uint32_t* steps,
+                         float* mean_out, float* act_out, float* logp_out, float* v_out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s[12];
+  for (int k = 0; k < 12; k++) s[k] = obs[(size_t)i * 12 + k];
+  if (v_out) {
+    v_out[i] = critic_value(W, s);
+    return;
+  }
+  float mean[4], a[4], lp[4];
+  actor_mean(W, s, mean);
+  uint32_t gid = env_ids ? (uint32_t)env_ids[i] : (uint32_t)(P.env_offset + i);
+  uint32_t t = steps ? steps[i] : 0u;
+  sample_actions(P, lp_const, gid, t, mean, a, lp);
+  for (int d = 0; d < 4; d++) {
+    if (mean_out) mean_out[(size_t)i * 4 + d] = mean[d];
+    if (act_out) act_out[(size_t)i * 4 + d] = a[d];
+    if (logp_out) logp_out[(size_t)i * 4 + d] = lp[d];
+  }
+}
+
+// returns / advantages (PPOAgent.cs:175-189, 414-498), one lane per env, reverse scan
+// over the horizon; done[t] ends an episode at t.
+__global__ void k_returns(int n, int T, int use_gae, float gamma, float lambda,
+                          const float* __restrict__ r, const float* __restrict__ v,
+                          const uint8_t* __restrict__ done, float* ret, float* adv) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  if (!use_gae) {
+    float disc = 0.0f;
+    for (int t = T - 1; t >= 0; t--) {
+      size_t i = (size_t)t * n + e;
+      if (done[i]) disc = 0.0f;
+      disc = r[i] + (disc * gamma);
+      ret[i] = disc;
+      adv[i] = disc - v[i];
+    }
+  } else {
+    float nextGae = 0.0f, nextValue = 0.0f;
+    for (int t = T - 1; t >= 0; t--) {
+      size_t i = (size_t)t * n + e;
+      if (done[i]) nextValue = 0.0f;
+      float cur = v[i];
+      float delta = r[i] + (gamma * nextValue) - cur;
+      nextValue = cur;
+      float gae = delta + (gamma * lambda * nextGae);  // reference quirk: nextGae stays 0
+      adv[i] = gae;
+      ret[i] = gae + cur;
+    }
+  }
+}
+
+// explicit instantiations used by the host
+template __global__ void k_env_step<false, false, false>(EnvParams, StepArgs);
+template __global__ void k_env_step<false, false, true>(EnvParams, StepArgs);
+template __global__ void k_env_step<true, false, false>(EnvParams, StepArgs);
+template __global__ void k_env_step<true, true, false>(EnvParams, StepArgs);
+
+}  // namespace wk
+
+// host-side launch shims (C++ linkage, used by wk_api.cpp)
+namespace wk {
+hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
+  dim3 blk(64), grd((P.n_env + 63) / 64);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((k_env_step<false, false, false>), grd, blk, 0, s, P, A); break;
+    case 1: hipLaunchKernelGGL((k_env_step<false, false, true>), grd, blk, 0, s, P, A); break;
+    case 2: hipLaunchKernelGGL((k_env_step<true, false, false>), grd, blk, 0, s, P, A); break;
+    default: hipLaunchKernelGGL((k_env_step<true, true, false>), grd, blk, 0, s, P, A); break;
+  }
+  return hipGetLastError();
+}
+hipError_t launch_env_init(const EnvParams& P, float* st, const float* dx, const uint8_t* mask,
+                           int post, hipStream_t s) {
+  hipLaunchKernelGGL(k_env_init, dim3((P.n_env + 255) / 256), dim3(256), 0, s, P, st, dx, mask, post);
+  return hipGetLastError();
+}
+hipError_t launch_get_obs(const EnvParams& P, const float* st, float* obs, hipStream_t s) {
+  hipLaunchKernelGGL(k_get_obs, dim3((P.n_env + 255) / 256), dim3(256), 0, s, P, st, obs);
+  return hipGetLastError();
+}
+hipError_t launch_policy(const EnvParams& P, const float* W, float lp_const, int n,
+                         const float* obs, const int32_t* env_ids, const uint32_t* steps,
+                         float* mean, float* act, float* logp, float* v, hipStream_t s) {
+  hipLaunchKernelGGL(k_policy, dim3((n + 63) / 64), dim3(64), 0, s, P, W, lp_const, n, obs,
+                     env_ids, steps, mean, act, logp, v);
+  return hipGetLastError();
+}
+hipError_t launch_returns(int n, int T, int use_gae, float gamma, float lambda, const float* r,
+                          const float* v, const uint8_t* d, float* ret, float* adv,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(k_returns, dim3((n + 255) / 256), dim3(256), 0, s, n, T, use_gae, gamma,
+                     lambda, r, v, d, ret, adv);
+  return hipGetLastError();
+}
+}  // namespace wk

@@ -1,0 +1,370 @@
+// wk_ppo.hip -- PPO clipped-surrogate gradient, deterministic reduction and Adam (gfx950).
+//
+// k_ppo_grad restates PPOAgent.Train(Batch) (Walker/PPO/PPOAgent.cs:218-346) for a
+// minibatch: per sample the critic and actor forward passes with cache
+// (NeuralNetwork.FeedForward, NeuralNetwork.cs:52-64), the per-dimension clipped ratio
+// gradient (PPOAgent.cs:248-326), and NeuralNetwork.FeedBack (NeuralNetwork.cs:67-82,
+// DenseLayer.FeedBack DenseLayer.cs:103-120, ActivationLayer.FeedBack
+// ActivationLayer.cs:18-21) accumulating dW/db.  Mapping: one wave per sample stream,
+// lane j = neuron j of every 64-wide layer; weights staged once per block in LDS in the
+// two orientations the forward and backward passes read (both conflict-free); per-wave
+// accumulators stay in VGPRs; waves fold into one LDS slab in wave order, blocks write
+// partial slabs that k_grad_reduce sums in block order (no atomics: bit-reproducible).
+// Within a wave the samples are visited in minibatch order, so a single-wave launch
+// reproduces the reference's sequential accumulation exactly.
+#include "wk_common.h"
+#include "wk_kernels.h"
+
+namespace wk {
+
+#define DEV __device__ __forceinline__
+
+DEV float net_maxf_(float x, float y) {
+  if (x != y) { if (!__builtin_isnan(x)) return y < x ? x : y; return x; }
+  return __builtin_signbit(y) ? x : y;
+}
+DEV float lrelu(float z) { return net_maxf_(0.2f * z, z); }
+DEV float dlrelu(float z) { return z < 0.0f ? 0.2f : 1.0f; }
+
+// LDS weight image (floats)
+enum : int {
+  L_AW1 = 0,                  // [64][13] actor W1 (row j padded)
+  L_CW1 = L_AW1 + 64 * 13,    // [64][13] critic W1
+  L_AW2T = L_CW1 + 64 * 13,   // [64 k][64 j] actor W2 transposed (forward)
+  L_AW2 = L_AW2T + 4096,      // [64 j][64 k] actor W2 (backward)
+  L_AW3 = L_AW2 + 4096,       // [4][65]
+  L_CW2 = L_AW3 + 4 * 65,     // [64]
+  L_AB1 = L_CW2 + 64, L_AB2 = L_AB1 + 64, L_CB1 = L_AB2 + 64, L_AB3 = L_CB1 + 64,
+  L_CB2 = L_AB3 + 4,
+  L_WEND = L_CB2 + 4
+};
+
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_ppo_grad(GradArgs g) {
+  extern __shared__ float lds[];
+  float* wl = lds;                         // weights
+  float* slab = lds + L_WEND;              // [SLAB] block accumulation
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* wv = slab + SLAB + wave * (64 * 4 + 24);  // per-wave scratch
+  float* h1s = wv;
+  float* h2s = wv + 64;
+  float* hc1s = wv + 128;
+  float* gz2s = wv + 192;
+  float* smp = wv + 256;                   // 12 s + 4 a + 4 lpo + G + A (+pad)
+
+  // ---- stage weights ----
+  for (int i = threadIdx.x; i < 64 * 12; i += 64 * WPB) {
+    int j = i / 12, k = i % 12;
+    wl[L_AW1 + j * 13 + k] = g.W[OFF_A_W1 + i];
+    wl[L_CW1 + j * 13 + k] = g.W[OFF_C_W1 + i];
+  }
+  for (int i = threadIdx.x; i < 4096; i += 64 * WPB) {
+    int j = i >> 6, k = i & 63;
+    float w = g.W[OFF_A_W2 + i];
+    wl[L_AW2 + i] = w;
+    wl[L_AW2T + k * 64 + j] = w;
+  }
+  for (int i = threadIdx.x; i < 256; i += 64 * WPB) wl[L_AW3 + (i >> 6) * 65 + (i & 63)] = g.W[OFF_A_W3 + i];
+  for (int i = threadIdx.x; i < 64; i += 64 * WPB) {
+    wl[L_CW2 + i] = g.W[OFF_C_W2 + i];
+    wl[L_AB1 + i] = g.W[OFF_A_B1 + i];
+    wl[L_AB2 + i] = g.W[OFF_A_B2 + i];
+    wl[L_CB1 + i] = g.W[OFF_C_B1 + i];
+  }
+  if (threadIdx.x < 4) wl[L_AB3 + threadIdx.x] = g.W[OFF_A_B3 + threadIdx.x];
+  if (threadIdx.x == 0) wl[L_CB2] = g.W[OFF_C_B2];
+  for (int i = threadIdx.x; i < SLAB; i += 64 * WPB) slab[i] = 0.0f;
+  __syncthreads();
+
+  // ---- per-lane accumulators (lane = neuron) ----
+  float dW2[64];
+#pragma unroll
+  for (int k = 0; k < 64; k++) dW2[k] = 0.0f;
+  float dW1[12], dWc1[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) { dW1[i] = 0.0f; dWc1[i] = 0.0f; }
+  float dW3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, db3[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  float db1 = 0.0f, db2 = 0.0f, dbc1 = 0.0f, dWc2 = 0.0f, dbc2 = 0.0f;
+  float diagC = 0.0f, diagA = 0.0f, skipped = 0.0f;
+
+  const float aw1_b = wl[L_AB1 + lane], aw2_b = wl[L_AB2 + lane], cw1_b = wl[L_CB1 + lane];
+  const float cw2_l = wl[L_CW2 + lane];
+  const float cb2 = wl[L_CB2];
+  const int first = (blockIdx.x * WPB + wave) * g.spw;
+
+#pragma unroll 1
+  for (int q = 0; q < g.spw; q++) {
+    const int pos = first + q;
+    if (pos >= g.samples) break;  // wave-uniform
+    // ---- gather the sample (CreateBatches, PPOAgent.cs:512-533) ----
+    uint32_t idx = g.base + (uint32_t)pos;
+    if (g.use_perm) idx = perm_apply(idx, g.pk);
+    if (lane < 12) smp[lane] = g.states[(size_t)idx * 12 + lane];
+    else if (lane < 16) smp[lane] = g.actions[(size_t)idx * 4 + lane - 12];
+    else if (lane < 20) smp[lane] = g.logp_old[(size_t)idx * 4 + lane - 16];
+    else if (lane == 20) smp[20] = g.returns[idx];
+    else if (lane == 21) smp[21] = g.adv[idx];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    float s[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = smp[i];
+
+    // ---- layer 1 (actor and critic): z_j = (sum_k W[j][k] s_k) + b_j ----
+    float z1 = 0.0f, zc1 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      z1 = z1 + wl[L_AW1 + lane * 13 + k] * s[k];
+      zc1 = zc1 + wl[L_CW1 + lane * 13 + k] * s[k];
+    }
+    z1 = z1 + aw1_b;
+    zc1 = zc1 + cw1_b;
+    const float h1 = lrelu(z1), hc1 = lrelu(zc1);
+    h1s[lane] = h1;
+    hc1s[lane] = hc1;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // ---- actor layer 2 ----
+    float z2 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 64; k++) z2 = z2 + wl[L_AW2T + k * 64 + lane] * h1s[k];
+    z2 = z2 + aw2_b;
+    const float h2 = lrelu(z2);
+    h2s[lane] = h2;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // ---- critic output (all lanes, sequential over k) ----
+    float V = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 64; k++) V = V + wl[L_CW2 + k] * hc1s[k];
+    V = V + cb2;
+    // ---- actor output: lanes 0..3 own one action dimension each ----
+    const int d = lane & 3;
+    float z3 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 64; k++) z3 = z3 + wl[L_AW3 + d * 65 + k] * h2s[k];
+    z3 = z3 + wl[L_AB3 + d];
+    const float mean = tanhf(z3);
+    // ---- PPO derivative (PPOAgent.cs:234-326), per dimension ----
+    const float A = smp[21];
+    float criticLoss = 2.0f * (V - smp[20]);
+    const float act = smp[12 + d], lpo = smp[16 + d];
+    float fr = (act - mean) / g.std_;
+    fr *= fr;
+    fr /= 2.0f;
+    const float lp = g.lp_const - fr;
+    const float r = expf(lp - lpo);
+    const float cr = r >= g.upper ? g.upper : (r <= g.lower ? g.lower : r);
+    const float cra = cr * A, ra = r * A;
+    const float partA = (ra <= cra ? 1.0f : 0.0f) * A;
+    const float partB = (cra < ra ? 1.0f : 0.0f) * A;
+    const float partC = (r >= g.lower && r <= g.upper) ? 1.0f : 0.0f;
+    float l = partA + (partB * partC);
+    l = l * -1.0f;
+    const float eo = expf(lpo);
+    const bool zero_div = (lane < 4) && (eo == 0.0f);
+    const float lcd = l / eo;
+    const float prob = expf(lp);
+    const float frac = (act - mean) / (g.std_ * g.std_);
+    float actorLoss = (prob * frac) * lcd;
+    const bool skip = __any(zero_div);  // Matrix.HadamardDivision throws -> continue
+    if (skip) {
+      skipped += 1.0f;
+      continue;
+    }
+    criticLoss /= g.b_div;
+    actorLoss = actorLoss / g.b_div;
+    // broadcast the 4 per-dimension values
+    const float al0 = __shfl(actorLoss, 0), al1 = __shfl(actorLoss, 1);
+    const float al2 = __shfl(actorLoss, 2), al3 = __shfl(actorLoss, 3);
+    diagC += criticLoss;
+    diagA += ((((0.0f + al0) + al1) + al2) + al3) / 4.0f;
+    // ---- actor backward ----
+    const float th = tanhf(z3);
+    const float gz3 = actorLoss * (1.0f - (th * th));
+    float gz3v[4];
+    gz3v[0] = __shfl(gz3, 0); gz3v[1] = __shfl(gz3, 1);
+    gz3v[2] = __shfl(gz3, 2); gz3v[3] = __shfl(gz3, 3);
+#pragma unroll
+    for (int dd = 0; dd < 4; dd++) {
+      dW3[dd] = dW3[dd] + gz3v[dd] * h2;   // lane = column k of W3
+      db3[dd] = db3[dd] + gz3v[dd];
+    }
+    float gh2 = 0.0f;
+#pragma unroll
+    for (int dd = 0; dd < 4; dd++) gh2 = gh2 + wl[L_AW3 + dd * 65 + lane] * gz3v[dd];
+    const float gz2 = gh2 * dlrelu(z2);
+    gz2s[lane] = gz2;
+    db2 = db2 + gz2;
+#pragma unroll
+    for (int k = 0; k < 64; k++) dW2[k] = dW2[k] + gz2 * h1s[k];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    float gh1 = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 64; j++) gh1 = gh1 + wl[L_AW2 + j * 64 + lane] * gz2s[j];
+    const float gz1 = gh1 * dlrelu(z1);
+    db1 = db1 + gz1;
+#pragma unroll
+    for (int i = 0; i < 12; i++) dW1[i] = dW1[i] + gz1 * s[i];
+    // ---- critic backward ----
+    dWc2 = dWc2 + criticLoss * hc1;
+    dbc2 = dbc2 + criticLoss;
+    const float ghc1 = 0.0f + cw2_l * criticLoss;
+    const float gzc1 = ghc1 * dlrelu(zc1);
+    dbc1 = dbc1 + gzc1;
+#pragma unroll
+    for (int i = 0; i < 12; i++) dWc1[i] = dWc1[i] + gzc1 * s[i];
+  }
+
+  // ---- fold waves into the block slab in wave order ----
+#pragma unroll 1
+  for (int w = 0; w < WPB; w++) {
+    if (w == wave) {
+      const int j = lane;
+#pragma unroll
+      for (int i = 0; i < 12; i++) {
+        slab[OFF_C_W1 + j * 12 + i] += dWc1[i];
+        slab[OFF_A_W1 + j * 12 + i] += dW1[i];
+      }
+      slab[OFF_C_B1 + j] += dbc1;
+      slab[OFF_C_W2 + j] += dWc2;
+      slab[OFF_A_B1 + j] += db1;
+#pragma unroll
+      for (int k = 0; k < 64; k++) slab[OFF_A_W2 + j * 64 + k] += dW2[k];
+      slab[OFF_A_B2 + j] += db2;
+#pragma unroll
+      for (int dd = 0; dd < 4; dd++) slab[OFF_A_W3 + dd * 64 + j] += dW3[dd];
+      if (lane == 0) {
+        slab[OFF_C_B2] += dbc2;
+#pragma unroll
+        for (int dd = 0; dd < 4; dd++) slab[OFF_A_B3 + dd] += db3[dd];
+        slab[NPARAM] += diagC;
+        slab[NPARAM + 1] += diagA;
+        slab[NPARAM + 2] += skipped;
+      }
+    }
+    __syncthreads();
+  }
+  float* out = g.partial + (size_t)blockIdx.x * SLAB;
+  for (int i = threadIdx.x; i < SLAB; i += 64 * WPB) out[i] = slab[i];
+}
+
+// sum block slabs in block order: grad[p] = ((0 + P0[p]) + P1[p]) + ...
+__global__ void k_grad_reduce(const float* __restrict__ partial, int nblocks, float* grad) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= SLAB) return;
+  float acc = 0.0f;
+  for (int b = 0; b < nblocks; b++) acc = acc + partial[(size_t)b * SLAB + p];
+  grad[p] = acc;
+}
+
+// DenseLayer.Adam (DenseLayer.cs:125-159), elementwise over all 6149 parameters
+__global__ void k_adam(AdamArgs a) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= NPARAM) return;
+  const float gr = a.grad[p];
+  float m = (gr * a.c1) + (a.m[p] * a.beta1);
+  float v = (a.v[p] * a.beta2) + ((gr * gr) * a.c2);
+  a.m[p] = m;
+  a.v[p] = v;
+  float mh = m / a.bc1;
+  float vh = v / a.bc2;
+  float den = __fsqrt_rn(vh) + a.eps;
+  a.W[p] = a.W[p] - ((mh / den) * a.alpha);
+}
+
+// Normalize (PPOAgent.cs:461-472): LINQ Average/Sum accumulate in double
+__global__ void k_normalize(float* x, int n, float eps_clip) {
+  __shared__ double red[1024];
+  __shared__ float mean_s, std_s;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += (double)x[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) mean_s = (float)(red[0] / (double)n);
+  __syncthreads();
+  const float mean = mean_s;
+  double ss = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    double dv = (double)(x[i] - mean);
+    ss += dv * dv;
+  }
+  __syncthreads();
+  red[threadIdx.x] = ss;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) std_s = (float)sqrt(red[0] / (double)n);
+  __syncthreads();
+  const float sd = std_s;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    float v = x[i] - mean;
+    x[i] = v / (sd + eps_clip);
+  }
+}
+
+// Xavier-normal init (Matrix.FromXavier, Matrix.cs:59-80) on the device
+__global__ void k_xavier(float* W, uint64_t seed) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= NPARAM) return;
+  // (offset, rows, cols, global dense-layer index) of the five dense layers
+  const int offs[5] = {OFF_C_W1, OFF_C_W2, OFF_A_W1, OFF_A_W2, OFF_A_W3};
+  const int rows[5] = {64, 1, 64, 64, 4}, cols[5] = {12, 64, 12, 64, 64};
+  float v = 0.0f;
+#pragma unroll
+  for (int l = 0; l < 5; l++) {
+    const int n = rows[l] * cols[l];
+    if (p >= offs[l] && p < offs[l] + n) {
+      const int k = p - offs[l];
+      U4 o = philox(seed, (uint32_t)k, (uint32_t)l, 0, ST_XAVIER);
+      float u1 = next_double_f(o.x, o.y), u2 = next_double_f(o.z, o.w);
+      if (u1 == 0.0f) u1 = 1.0f;
+      const float PI_F = 3.14159265358979323846f;
+      float std_ = __fsqrt_rn(2.0f / (float)(rows[l] + cols[l]));
+      float z = __fsqrt_rn(-2.0f * logf(u1)) * sinf(2.0f * PI_F * u2);
+      v = 0.0f + (std_ * z);
+    }
+  }
+  W[p] = v;
+}
+
+hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t s) {
+  const size_t lds = sizeof(float) * (L_WEND + SLAB + wpb * (64 * 4 + 24));
+  static bool attr_set = false;
+  if (!attr_set) {  // > 64 KiB of dynamic LDS (gfx950 CU has 160 KiB)
+    hipFuncSetAttribute((const void*)k_ppo_grad<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_ppo_grad<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  if (wpb == 1) {
+    hipLaunchKernelGGL((k_ppo_grad<1>), dim3(nblocks), dim3(64), lds, s, g);
+  } else {
+    hipLaunchKernelGGL((k_ppo_grad<4>), dim3(nblocks), dim3(256), lds, s, g);
+  }
+  return hipGetLastError();
+}
+hipError_t launch_grad_reduce(const float* partial, int nblocks, float* grad, hipStream_t s) {
+  hipLaunchKernelGGL(k_grad_reduce, dim3((SLAB + 255) / 256), dim3(256), 0, s, partial, nblocks, grad);
+  return hipGetLastError();
+}
+hipError_t launch_adam(const AdamArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_adam, dim3((NPARAM + 255) / 256), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_normalize(float* x, int n, float eps, hipStream_t s) {
+  hipLaunchKernelGGL(k_normalize, dim3(1), dim3(1024), 0, s, x, n, eps);
+  return hipGetLastError();
+}
+hipError_t launch_xavier(float* W, uint64_t seed, hipStream_t s) {
+  hipLaunchKernelGGL(k_xavier, dim3((NPARAM + 255) / 256), dim3(256), 0, s, W, seed);
+  return hipGetLastError();
+}
+
+}  // namespace wk

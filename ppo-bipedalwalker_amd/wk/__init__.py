@@ -1,0 +1,410 @@
+"""ctypes binding of libwk.so (include/wk_api.h) -- the MI355X batched walker engine.
+
+This is plumbing for tests and bench.py: every call goes straight to the C ABI and
+from there to HIP kernels on gfx950.  There is no CPU fallback: if libwk.so is
+missing or no GPU is visible, construction raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libwk.so")
+
+STATE_FLOATS = 112
+NPARAM = 6149
+NPARAM_CRITIC = 897
+NPAIRS = 9
+ST_TORQUE, ST_POS, ST_PREV, ST_STEPS, ST_POSTRESET, ST_TERMINAL, ST_EPISODES = (
+    100, 104, 106, 108, 109, 110, 111)
+MATERIALS = {"Carpet": 0, "Ice": 1, "Rubber": 2, "Metal": 3, "Wood": 4, "Paper": 5,
+             "Titanium": 6, "SuperRubber": 7}
+
+# every symbol include/wk_api.h declares (checked by tests/test_boundary.py)
+EXPORTS = [
+    "wk_config_defaults", "wk_version", "wk_create", "wk_destroy", "wk_last_error", "wk_sync",
+    "wk_num_envs", "wk_reset", "wk_set_materials", "wk_set_offsets", "wk_step",
+    "wk_step_device", "wk_step_traced", "wk_get_obs", "wk_get_state", "wk_set_state",
+    "wk_get_body_view", "wk_get_weights", "wk_set_weights", "wk_get_adam", "wk_set_adam",
+    "wk_policy_sample", "wk_value", "wk_rollout", "wk_rollout_stats_get", "wk_get_trajectory",
+    "wk_set_trajectory", "wk_compute_returns", "wk_ppo_update", "wk_train_batch",
+    "wk_comm_unique_id", "wk_comm_init", "wk_allreduce_test", "wk_profile_enable",
+    "wk_profile_get", "wk_profile_reset",
+]
+
+
+class WkConfig(C.Structure):
+    """wk_config: Hyperparameters.cs:80-121 names and defaults + batched extensions."""
+    _fields_ = [
+        ("GameSpeed", C.c_int), ("Iterations", C.c_int), ("MaxTimesteps", C.c_int),
+        ("RoughFloor", C.c_int), ("Epochs", C.c_int), ("BatchSize", C.c_int),
+        ("UseGAE", C.c_int), ("NormalizeAdvantages", C.c_int), ("Gamma", C.c_float),
+        ("Lambda", C.c_float), ("Epsilon", C.c_float), ("LogStandardDeviation", C.c_float),
+        ("Alpha", C.c_float), ("Beta1", C.c_float), ("Beta2", C.c_float),
+        ("AdamEpsilon", C.c_float), ("CriticNeuralNetwork", C.c_char_p),
+        ("ActorNeuralNetwork", C.c_char_p), ("DeltaTime", C.c_float), ("Horizon", C.c_int),
+        ("Minibatch", C.c_int), ("MinibatchGlobal", C.c_int), ("EnvOffset", C.c_int),
+        ("RandomizeStart", C.c_int), ("RandomizeMaterial", C.c_int),
+    ]
+
+
+class PairTrace(C.Structure):
+    _fields_ = [("aabb_hit", C.c_uint8 * 9), ("sat_hit", C.c_uint8 * 9),
+                ("n_contacts", C.c_uint8 * 9), ("pad", C.c_uint8 * 5),
+                ("normal", (C.c_float * 2) * 9), ("depth", C.c_float * 9)]
+
+
+TRACE_DTYPE = np.dtype([("aabb_hit", np.uint8, 9), ("sat_hit", np.uint8, 9),
+                        ("n_contacts", np.uint8, 9), ("pad", np.uint8, 5),
+                        ("normal", np.float32, (9, 2)), ("depth", np.float32, 9)])
+assert TRACE_DTYPE.itemsize == C.sizeof(PairTrace) == 140
+
+
+class BodyView(C.Structure):
+    _fields_ = [("n_vertices", C.c_int), ("vertices", (C.c_float * 2) * 6),
+                ("centroid", C.c_float * 2), ("linear_velocity", C.c_float * 2),
+                ("angular_velocity", C.c_float), ("angle", C.c_float), ("collided", C.c_int),
+                ("is_static", C.c_int)]
+
+
+class PpoArgs(C.Structure):
+    _fields_ = [("epochs", C.c_int), ("minibatch", C.c_int), ("minibatch_global", C.c_int),
+                ("update_index", C.c_uint32)]
+
+
+class RolloutStats(C.Structure):
+    _fields_ = [("reward_sum", C.c_double), ("episodes", C.c_int64), ("env_steps", C.c_int64),
+                ("fault_or", C.c_uint32), ("pad", C.c_int32)]
+
+
+class Profile(C.Structure):
+    _fields_ = [("physics_ms", C.c_double), ("physics_launches", C.c_int64),
+                ("physics_env_steps", C.c_int64), ("grad_ms", C.c_double),
+                ("grad_launches", C.c_int64), ("reduce_ms", C.c_double),
+                ("reduce_launches", C.c_int64), ("adam_ms", C.c_double),
+                ("adam_launches", C.c_int64), ("allreduce_ms", C.c_double),
+                ("allreduce_calls", C.c_int64), ("returns_ms", C.c_double),
+                ("returns_launches", C.c_int64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load libwk.so (raises OSError if it was not built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise OSError(f"libwk.so not built at {p}: run __graft_entry__.build() "
+                      "(or make -C ppo-bipedalwalker_amd)")
+    # PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64 / librccl with the same
+    # SONAMEs as /opt/rocm.  Loading torch first makes libwk.so bind to those copies, so
+    # one process has exactly one HIP runtime (torch.cuda.synchronize() then also covers
+    # libwk's stream).  Loading libwk first would pull in a second runtime under torch.
+    try:
+        import torch  # noqa: F401
+    except Exception:  # torch is plumbing only; libwk.so stands alone without it
+        pass
+    lib = C.CDLL(p)
+    P, I, F, U32, U64 = C.c_void_p, C.c_int, C.c_float, C.c_uint32, C.c_uint64
+    fp = C.POINTER(C.c_float)
+    sig = {
+        "wk_config_defaults": (None, [C.POINTER(WkConfig)]),
+        "wk_version": (C.c_char_p, []),
+        "wk_create": (I, [C.POINTER(WkConfig), I, I, U64, C.POINTER(P)]),
+        "wk_destroy": (I, [P]),
+        "wk_last_error": (C.c_char_p, [P]),
+        "wk_sync": (I, [P]),
+        "wk_num_envs": (I, [P]),
+        "wk_reset": (I, [P, P]),
+        "wk_set_materials": (I, [P, P]),
+        "wk_set_offsets": (I, [P, P]),
+        "wk_step": (I, [P, P, I, P, P, P, P]),
+        "wk_step_device": (I, [P, P, I, P, P, P, P]),
+        "wk_step_traced": (I, [P, P, P]),
+        "wk_get_obs": (I, [P, P]),
+        "wk_get_state": (I, [P, P]),
+        "wk_set_state": (I, [P, P]),
+        "wk_get_body_view": (I, [P, I, I, C.POINTER(BodyView)]),
+        "wk_get_weights": (I, [P, P]),
+        "wk_set_weights": (I, [P, P]),
+        "wk_get_adam": (I, [P, P, P, C.POINTER(C.c_int)]),
+        "wk_set_adam": (I, [P, P, P, I]),
+        "wk_policy_sample": (I, [P, I, P, P, P, P, P, P]),
+        "wk_value": (I, [P, I, P, P]),
+        "wk_rollout": (I, [P, I]),
+        "wk_rollout_stats_get": (I, [P, C.POINTER(RolloutStats)]),
+        "wk_get_trajectory": (I, [P, P, P, P, P, P, P, P, P]),
+        "wk_set_trajectory": (I, [P, I, P, P, P, P, P, P]),
+        "wk_compute_returns": (I, [P]),
+        "wk_ppo_update": (I, [P, C.POINTER(PpoArgs), fp, fp]),
+        "wk_train_batch": (I, [P, I, F, P, P, P, P, P, fp, fp, P, I, C.POINTER(C.c_int)]),
+        "wk_comm_unique_id": (I, [P]),
+        "wk_comm_init": (I, [P, I, I, P]),
+        "wk_allreduce_test": (I, [P, P, I]),
+        "wk_profile_enable": (I, [P, I]),
+        "wk_profile_get": (I, [P, C.POINTER(Profile)]),
+        "wk_profile_reset": (I, [P]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _ = U32
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _f32(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    if shape is not None:
+        a = a.reshape(shape)
+    return a
+
+
+class WkError(RuntimeError):
+    pass
+
+
+def default_config(**overrides):
+    lib = load_library()
+    c = WkConfig()
+    lib.wk_config_defaults(C.byref(c))
+    for k, v in overrides.items():
+        if not hasattr(c, k):
+            raise KeyError(f"unknown wk_config field {k}")
+        if isinstance(v, str):
+            v = v.encode()
+        setattr(c, k, v)
+    return c
+
+
+class Engine:
+    """One wk_ctx: n_env walkers on one GPU."""
+
+    def __init__(self, n_env, seed=20250905, device=0, **cfg):
+        self.lib = load_library()
+        self.cfg = default_config(**cfg)
+        self.n = int(n_env)
+        self.seed = int(seed)
+        h = C.c_void_p()
+        rc = self.lib.wk_create(C.byref(self.cfg), int(device), self.n, self.seed, C.byref(h))
+        if rc != 0:
+            raise WkError(f"wk_create failed ({rc}): {self.lib.wk_last_error(None).decode()}")
+        self.h = h
+
+    # -- plumbing --
+    def _chk(self, rc, what):
+        if rc != 0:
+            raise WkError(f"{what} failed ({rc}): {self.lib.wk_last_error(self.h).decode()}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.wk_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def sync(self):
+        self._chk(self.lib.wk_sync(self.h), "wk_sync")
+
+    # -- environment --
+    def reset(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        self._chk(self.lib.wk_reset(self.h, _ptr(m)), "wk_reset")
+
+    def set_materials(self, mat):
+        m = np.ascontiguousarray(mat, dtype=np.int32)
+        self._chk(self.lib.wk_set_materials(self.h, _ptr(m)), "wk_set_materials")
+
+    def set_offsets(self, dx):
+        d = _f32(dx)
+        self._chk(self.lib.wk_set_offsets(self.h, _ptr(d)), "wk_set_offsets")
+
+    def step(self, actions=None, k=1):
+        """k env-steps; actions [k, n, 4] (unclipped) or None to sample from the policy."""
+        a = None if actions is None else _f32(actions, (k, self.n, 4))
+        obs = np.empty((k, self.n, 12), np.float32)
+        rew = np.empty((k, self.n), np.float32)
+        done = np.empty((k, self.n), np.uint8)
+        fault = np.empty(self.n, np.uint32)
+        self._chk(self.lib.wk_step(self.h, _ptr(a), int(k), _ptr(obs), _ptr(rew), _ptr(done),
+                                   _ptr(fault)), "wk_step")
+        return obs, rew, done, fault
+
+    def step_device(self, d_actions, k, d_obs, d_rew, d_done, d_fault):
+        """Device-pointer variant (ints or None) on the context's stream; no sync."""
+        self._chk(self.lib.wk_step_device(self.h, d_actions, int(k), d_obs, d_rew, d_done,
+                                          d_fault), "wk_step_device")
+
+    def step_traced(self, actions):
+        a = _f32(actions, (self.n, 4))
+        tr = np.zeros((self.n, self.cfg.Iterations), TRACE_DTYPE)
+        self._chk(self.lib.wk_step_traced(self.h, _ptr(a), _ptr(tr)), "wk_step_traced")
+        return tr
+
+    def get_obs(self):
+        o = np.empty((self.n, 12), np.float32)
+        self._chk(self.lib.wk_get_obs(self.h, _ptr(o)), "wk_get_obs")
+        return o
+
+    def get_state(self):
+        s = np.empty((self.n, STATE_FLOATS), np.float32)
+        self._chk(self.lib.wk_get_state(self.h, _ptr(s)), "wk_get_state")
+        return s
+
+    def set_state(self, s):
+        s = _f32(s, (self.n, STATE_FLOATS))
+        self._chk(self.lib.wk_set_state(self.h, _ptr(s)), "wk_set_state")
+
+    def body_view(self, env, body):
+        v = BodyView()
+        self._chk(self.lib.wk_get_body_view(self.h, int(env), int(body), C.byref(v)),
+                  "wk_get_body_view")
+        return v
+
+    # -- policy --
+    def get_weights(self):
+        p = np.empty(NPARAM, np.float32)
+        self._chk(self.lib.wk_get_weights(self.h, _ptr(p)), "wk_get_weights")
+        return p
+
+    def set_weights(self, p):
+        p = _f32(p, (NPARAM,))
+        self._chk(self.lib.wk_set_weights(self.h, _ptr(p)), "wk_set_weights")
+
+    def get_adam(self):
+        m = np.empty(NPARAM, np.float32)
+        v = np.empty(NPARAM, np.float32)
+        t = C.c_int()
+        self._chk(self.lib.wk_get_adam(self.h, _ptr(m), _ptr(v), C.byref(t)), "wk_get_adam")
+        return m, v, t.value
+
+    def set_adam(self, m, v, t):
+        m = _f32(m, (NPARAM,))
+        v = _f32(v, (NPARAM,))
+        self._chk(self.lib.wk_set_adam(self.h, _ptr(m), _ptr(v), int(t)), "wk_set_adam")
+
+    def policy_sample(self, obs, env_ids=None, steps=None):
+        obs = _f32(obs)
+        n = obs.shape[0]
+        ids = None if env_ids is None else np.ascontiguousarray(env_ids, np.int32)
+        st = None if steps is None else np.ascontiguousarray(steps, np.uint32)
+        mean = np.empty((n, 4), np.float32)
+        act = np.empty((n, 4), np.float32)
+        lp = np.empty((n, 4), np.float32)
+        self._chk(self.lib.wk_policy_sample(self.h, n, _ptr(obs), _ptr(ids), _ptr(st), _ptr(mean),
+                                            _ptr(act), _ptr(lp)), "wk_policy_sample")
+        return mean, act, lp
+
+    def value(self, obs):
+        obs = _f32(obs)
+        v = np.empty(obs.shape[0], np.float32)
+        self._chk(self.lib.wk_value(self.h, obs.shape[0], _ptr(obs), _ptr(v)), "wk_value")
+        return v
+
+    # -- rollout / PPO --
+    def rollout(self, horizon=0):
+        self._chk(self.lib.wk_rollout(self.h, int(horizon)), "wk_rollout")
+
+    def rollout_stats(self):
+        s = RolloutStats()
+        self._chk(self.lib.wk_rollout_stats_get(self.h, C.byref(s)), "wk_rollout_stats_get")
+        return s
+
+    def get_trajectory(self, horizon):
+        n = self.n * horizon
+        out = dict(states=np.empty((horizon, self.n, 12), np.float32),
+                   actions=np.empty((horizon, self.n, 4), np.float32),
+                   logp=np.empty((horizon, self.n, 4), np.float32),
+                   rewards=np.empty((horizon, self.n), np.float32),
+                   dones=np.empty((horizon, self.n), np.uint8),
+                   values=np.empty((horizon, self.n), np.float32),
+                   returns=np.empty((horizon, self.n), np.float32),
+                   advantages=np.empty((horizon, self.n), np.float32))
+        assert n == out["rewards"].size
+        self._chk(self.lib.wk_get_trajectory(
+            self.h, _ptr(out["states"]), _ptr(out["actions"]), _ptr(out["logp"]),
+            _ptr(out["rewards"]), _ptr(out["dones"]), _ptr(out["values"]), _ptr(out["returns"]),
+            _ptr(out["advantages"])), "wk_get_trajectory")
+        return out
+
+    def set_trajectory(self, states, actions, logp, rewards, dones, values):
+        T = rewards.shape[0]
+        args = [_f32(states), _f32(actions), _f32(logp), _f32(rewards),
+                np.ascontiguousarray(dones, np.uint8), _f32(values)]
+        self._chk(self.lib.wk_set_trajectory(self.h, int(T), *[_ptr(a) for a in args]),
+                  "wk_set_trajectory")
+
+    def compute_returns(self):
+        self._chk(self.lib.wk_compute_returns(self.h), "wk_compute_returns")
+
+    def ppo_update(self, epochs=0, minibatch=0, minibatch_global=0, update_index=0):
+        a = PpoArgs(int(epochs), int(minibatch), int(minibatch_global), int(update_index))
+        cd, ad = C.c_float(), C.c_float()
+        self._chk(self.lib.wk_ppo_update(self.h, C.byref(a), C.byref(cd), C.byref(ad)),
+                  "wk_ppo_update")
+        return cd.value, ad.value
+
+    def train_batch(self, states, actions, logp_old, returns, adv, b_div=None, apply_adam=True):
+        s, a, l, r, v = (_f32(states), _f32(actions), _f32(logp_old), _f32(returns), _f32(adv))
+        B = r.shape[0]
+        grads = np.empty(NPARAM, np.float32)
+        cd, ad, sk = C.c_float(), C.c_float(), C.c_int()
+        self._chk(self.lib.wk_train_batch(
+            self.h, int(B), float(B if b_div is None else b_div), _ptr(s), _ptr(a), _ptr(l),
+            _ptr(r), _ptr(v), C.byref(cd), C.byref(ad), _ptr(grads), int(bool(apply_adam)),
+            C.byref(sk)), "wk_train_batch")
+        return grads, cd.value, ad.value, sk.value
+
+    # -- multi-GPU --
+    @staticmethod
+    def comm_unique_id():
+        lib = load_library()
+        buf = (C.c_uint8 * 128)()
+        rc = lib.wk_comm_unique_id(buf)
+        if rc != 0:
+            raise WkError(f"wk_comm_unique_id failed: {lib.wk_last_error(None).decode()}")
+        return bytes(buf)
+
+    def comm_init(self, rank, nranks, uid):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._chk(self.lib.wk_comm_init(self.h, int(rank), int(nranks), buf), "wk_comm_init")
+
+    def allreduce_test(self, x):
+        x = _f32(x).copy()
+        self._chk(self.lib.wk_allreduce_test(self.h, _ptr(x), x.size), "wk_allreduce_test")
+        return x
+
+    # -- profiling --
+    def profile_enable(self, on=True):
+        self._chk(self.lib.wk_profile_enable(self.h, int(bool(on))), "wk_profile_enable")
+
+    def profile_reset(self):
+        self._chk(self.lib.wk_profile_reset(self.h), "wk_profile_reset")
+
+    def profile(self):
+        p = Profile()
+        self._chk(self.lib.wk_profile_get(self.h, C.byref(p)), "wk_profile_get")
+        return p.as_dict()
