@@ -124,6 +124,10 @@ typedef struct wk_pair_trace {
   uint8_t pad[5];
   float normal[WK_NPAIRS][2];
   float depth[WK_NPAIRS];
+  float contact[WK_NPAIRS][2][2]; /* contact points (n_contacts valid) */
+  float impulse[WK_NPAIRS][2];    /* normal and friction impulse */
+  float joint_depth[4];           /* Joint.Step gap per joint (0 if < 0.1) */
+  float joint_impulse[4];
 } wk_pair_trace;
 
 /* one body of one env, for Renderer.RenderRigidObject / ConsoleRenderer */

@@ -27,7 +27,9 @@ class Hyper(C.Structure):
 
 TRACE_DTYPE = np.dtype([("aabb_hit", np.uint8, 9), ("sat_hit", np.uint8, 9),
                         ("n_contacts", np.uint8, 9), ("pad", np.uint8, 5),
-                        ("normal", np.float32, (9, 2)), ("depth", np.float32, 9)])
+                        ("normal", np.float32, (9, 2)), ("depth", np.float32, 9),
+                        ("contact", np.float32, (9, 2, 2)), ("impulse", np.float32, (9, 2)),
+                        ("joint_depth", np.float32, 4), ("joint_impulse", np.float32, 4)])
 
 _lib = None
 

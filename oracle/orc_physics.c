@@ -335,7 +335,7 @@ static void apply_impulses(body* A, body* B, v2 normal, float impulse, v2 rA, v2
   B->ang_vel = wb;
 }
 
-static void resolve_collision(body* A, body* B, const v2* cps, int ncp, v2 normal) {
+static void resolve_collision(body* A, body* B, const v2* cps, int ncp, v2 normal, float* jout) {
   if (ncp == 0) return;
   float e = net_maxf(A->restitution, B->restitution);
   float mu = net_minf(A->friction, B->friction);
@@ -345,16 +345,18 @@ static void resolve_collision(body* A, body* B, const v2* cps, int ncp, v2 norma
   calc_impulse(A, B, contact, 1.0f + e, normal, &rA, &rB, &j);
   v2 tangent = V(-normal.y, normal.x);
   calc_impulse(A, B, contact, mu, tangent, &rAF, &rBF, &jf);
+  if (jout) { jout[0] = j; jout[1] = jf; }
   apply_impulses(A, B, normal, j, rA, rB);
   apply_impulses(A, B, tangent, jf, rAF, rBF);
 }
 
-static void resolve_joint(body* A, body* B, v2 p0, v2 p1, v2 normal) {
+static float resolve_joint(body* A, body* B, v2 p0, v2 p1, v2 normal) {
   v2 contact = vdiv(vadd(p0, p1), 2.0f);
   v2 rA, rB;
   float j;
   calc_impulse(A, B, contact, 1.0f + 1.0f, normal, &rA, &rB, &j);
   apply_impulses(A, B, normal, j, rA, rB);
+  return j;
 }
 
 /* ---------------- RigidBody.Step / ResolveCollisions ---------------- */
@@ -407,9 +409,13 @@ static void resolve_collisions(orc_env* e, int self, orc_pair_trace* tr) {
         tr->normal[pi][0] = normal.x;
         tr->normal[pi][1] = normal.y;
         tr->depth[pi] = depth;
+        for (int q = 0; q < ncp && q < 2; q++) {
+          tr->contact[pi][q][0] = cps[q].x;
+          tr->contact[pi][q][1] = cps[q].y;
+        }
       }
       move_objects(A, B, normal, depth);
-      resolve_collision(A, B, cps, ncp, normal);
+      resolve_collision(A, B, cps, ncp, normal, (tr && pi >= 0) ? tr->impulse[pi] : NULL);
     }
   }
 }
@@ -435,7 +441,7 @@ static void body_step(orc_env* e, int self, float dt, orc_pair_trace* tr) {
 }
 
 /* Joint.Step (Joint.cs:31-41) */
-static void joint_step(orc_env* e, joint* jn) {
+static void joint_step(orc_env* e, joint* jn, float* jd, float* jj) {
   body* A = &e->bodies[jn->a];
   body* B = &e->bodies[jn->b];
   v2 ab = vsub(B->v[jn->ib], A->v[jn->ia]);
@@ -444,17 +450,20 @@ static void joint_step(orc_env* e, joint* jn) {
   ab = vnormalize(ab);
   sk_move(A, vdiv(vmul(ab, depth), 2.0f));
   sk_move(B, vdiv(vmul(vneg(ab), depth), 2.0f));
-  resolve_joint(B, A, A->v[jn->ia], B->v[jn->ib], ab);
+  float j = resolve_joint(B, A, A->v[jn->ia], B->v[jn->ib], ab);
+  if (jd) *jd = depth;
+  if (jj) *jj = j;
 }
 
-void orc_env_joint_step(orc_env* e, int j) { joint_step(e, &e->joints[j]); }
+void orc_env_joint_step(orc_env* e, int j) { joint_step(e, &e->joints[j], NULL, NULL); }
 
 void orc_env_step_objects(orc_env* e, float deltaTime, orc_pair_trace* trace) {
   deltaTime = deltaTime / (float)e->h.Iterations;
   for (int i = 0; i < e->h.Iterations; i++) {
     orc_pair_trace* tr = trace ? &trace[i] : NULL;
     if (tr) memset(tr, 0, sizeof(*tr));
-    for (int j = 0; j < 4; j++) joint_step(e, &e->joints[j]);
+    for (int j = 0; j < 4; j++)
+      joint_step(e, &e->joints[j], tr ? &tr->joint_depth[j] : NULL, tr ? &tr->joint_impulse[j] : NULL);
     for (int k = 0; k < 6; k++) body_step(e, e->order[k], deltaTime, tr);
   }
 }
@@ -666,7 +675,7 @@ void orc_kat_pole_floor(float vy, float out[9]) {
     v2 cps[3];
     ncp = contact_points(p.v, 6, f.v, 4, normal, cps);
     move_objects(&p, &f, normal, depth);
-    resolve_collision(&p, &f, cps, ncp, normal);
+    resolve_collision(&p, &f, cps, ncp, normal, NULL);
   }
   out[0] = p.lin_vel.x; out[1] = p.lin_vel.y; out[2] = p.ang_vel;
   out[3] = p.centroid.x; out[4] = p.centroid.y; out[5] = (float)ncp;

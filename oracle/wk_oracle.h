@@ -51,6 +51,10 @@ typedef struct {
   uint8_t pad[5];
   float normal[ORC_NPAIRS][2];
   float depth[ORC_NPAIRS];
+  float contact[ORC_NPAIRS][2][2];
+  float impulse[ORC_NPAIRS][2];
+  float joint_depth[4];
+  float joint_impulse[4];
 } orc_pair_trace;
 
 /* materials (Materials/<Name>.cs) */

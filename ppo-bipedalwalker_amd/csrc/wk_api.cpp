@@ -402,7 +402,7 @@ int wk_step(wk_ctx* c, const float* actions, int k, float* obs, float* reward, u
 
 int wk_step_traced(wk_ctx* c, const float* actions, wk_pair_trace* trace) {
   if (!c || !actions || !trace) return WK_ERR_ARG;
-  static_assert(sizeof(wk_pair_trace) == 32 + 9 * 12, "trace layout");
+  static_assert(sizeof(wk_pair_trace) == sizeof(wk::PairTraceDev), "trace layout");
   const size_t n = c->n;
   const size_t b_act = sizeof(float) * 4 * n;
   const size_t b_tr = sizeof(wk_pair_trace) * n * c->cfg.Iterations;

@@ -21,9 +21,9 @@ DEV V2 vmul(V2 a, float s) { return mk(a.x * s, a.y * s); }
 DEV V2 vdiv(V2 a, float d) { float f = 1.0f / d; return mk(a.x * f, a.y * f); }
 DEV V2 vneg(V2 a) { return mk(-a.x, -a.y); }
 DEV float vdot(V2 a, V2 b) { return a.x * b.x + a.y * b.y; }
-DEV float vlen(V2 a) { return __fsqrt_rn(a.x * a.x + a.y * a.y); }
+DEV float vlen(V2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
 DEV V2 vnormalize(V2 a) {
-  float val = 1.0f / __fsqrt_rn(a.x * a.x + a.y * a.y);
+  float val = 1.0f / sqrtf(a.x * a.x + a.y * a.y);
   return mk(a.x * val, a.y * val);
 }
 

@@ -17,6 +17,10 @@ struct PairTraceDev {
   uint8_t pad[5];
   float normal[9][2];
   float depth[9];
+  float contact[9][2][2];
+  float impulse[9][2];
+  float joint_depth[4];
+  float joint_impulse[4];
 };
 
 struct StepArgs {

@@ -182,6 +182,8 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
     tr->normal[pi][0] = n.x;
     tr->normal[pi][1] = n.y;
     tr->depth[pi] = depth;
+    if (nc > 0) { tr->contact[pi][0][0] = c0.x; tr->contact[pi][0][1] = c0.y; }
+    if (nc > 1) { tr->contact[pi][1][0] = c1.x; tr->contact[pi][1][1] = c1.y; }
   }
   // MoveObjects (:99-113): A is never static here
   if (BSTATIC) {
@@ -201,13 +203,15 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   float j = calc_impulse(bA, bB, contact, 1.0f + e, n, rA, rB);
   V2 tangent = mk(-n.y, n.x);
   float jf = calc_impulse(bA, bB, contact, mu, tangent, rAF, rBF);
+  if (TRACE) { tr->impulse[pi][0] = j; tr->impulse[pi][1] = jf; }
   apply_impulses<BSTATIC>(bA, bB, n, j, rA, rB);
   apply_impulses<BSTATIC>(bA, bB, tangent, jf, rAF, rBF);
 }
 
 // Joint.Step (Objects/RigidBodies/Joint.cs:31-41); ResolveJoint swaps the bodies (:40)
-template <int NA, int NB, int IA, int IB>
-DEV void joint_step(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB) {
+template <int NA, int NB, int IA, int IB, bool TRACE>
+DEV void joint_step(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB,
+                    PairTraceDev* tr, int ji) {
   V2 ab = vsub(mk(B.x[IB], B.y[IB]), mk(A.x[IA], A.y[IA]));
   float depth = vlen(ab);
   if (depth < 0.1f) return;
@@ -219,6 +223,7 @@ DEV void joint_step(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, c
   Body bI{A.cx, A.cy, &dA, mA.im, mA.ii};  // manifold.BodyB = joint body A
   V2 rA, rB;
   float j = calc_impulse(bJ, bI, contact, 1.0f + 1.0f, ab, rA, rB);
+  if (TRACE) { tr->joint_depth[ji] = depth; tr->joint_impulse[ji] = j; }
   apply_impulses<false>(bJ, bI, ab, j, rA, rB);
 }
 
@@ -243,10 +248,10 @@ DEV void substep(EnvState& s, const Mat& mp, const Mat& mb, float dt, float adx,
   zero_dyn(dfl);
   const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};  // Metal, static: inverse mass/inertia 0
   // joints: [bodyJointLeft, bodyJointRight, leftJoint, rightJoint] (Walker.cs:182-187)
-  joint_step<5, 6, 1, 4>(s.body, s.dbody, mb, s.llu, s.dllu, mp);
-  joint_step<5, 6, 1, 4>(s.body, s.dbody, mb, s.rlu, s.drlu, mp);
-  joint_step<6, 6, 2, 3>(s.llu, s.dllu, mp, s.lll, s.dlll, mp);
-  joint_step<6, 6, 2, 3>(s.rlu, s.drlu, mp, s.rll, s.drll, mp);
+  joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.llu, s.dllu, mp, tr, 0);
+  joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.rlu, s.drlu, mp, tr, 1);
+  joint_step<6, 6, 2, 3, TRACE>(s.llu, s.dllu, mp, s.lll, s.dlll, mp, tr, 2);
+  joint_step<6, 6, 2, 3, TRACE>(s.rlu, s.drlu, mp, s.rll, s.drll, mp, tr, 3);
   // bodies in list order; the floor's own step is a no-op (static, zero velocity).
   // Episode 0 lists the floor last, every later episode first (Walker.cs:212-234):
   // that only changes the order of each leg segment's two candidate pairs.

@@ -270,7 +270,7 @@ __global__ void k_adam(AdamArgs a) {
   a.v[p] = v;
   float mh = m / a.bc1;
   float vh = v / a.bc2;
-  float den = __fsqrt_rn(vh) + a.eps;
+  float den = sqrtf(vh) + a.eps;
   a.W[p] = a.W[p] - ((mh / den) * a.alpha);
 }
 
@@ -327,8 +327,8 @@ __global__ void k_xavier(float* W, uint64_t seed) {
       float u1 = next_double_f(o.x, o.y), u2 = next_double_f(o.z, o.w);
       if (u1 == 0.0f) u1 = 1.0f;
       const float PI_F = 3.14159265358979323846f;
-      float std_ = __fsqrt_rn(2.0f / (float)(rows[l] + cols[l]));
-      float z = __fsqrt_rn(-2.0f * logf(u1)) * sinf(2.0f * PI_F * u2);
+      float std_ = sqrtf(2.0f / (float)(rows[l] + cols[l]));
+      float z = sqrtf(-2.0f * logf(u1)) * sinf(2.0f * PI_F * u2);
       v = 0.0f + (std_ * z);
     }
   }

@@ -52,13 +52,17 @@ class WkConfig(C.Structure):
 class PairTrace(C.Structure):
     _fields_ = [("aabb_hit", C.c_uint8 * 9), ("sat_hit", C.c_uint8 * 9),
                 ("n_contacts", C.c_uint8 * 9), ("pad", C.c_uint8 * 5),
-                ("normal", (C.c_float * 2) * 9), ("depth", C.c_float * 9)]
+                ("normal", (C.c_float * 2) * 9), ("depth", C.c_float * 9),
+                ("contact", ((C.c_float * 2) * 2) * 9), ("impulse", (C.c_float * 2) * 9),
+                ("joint_depth", C.c_float * 4), ("joint_impulse", C.c_float * 4)]
 
 
 TRACE_DTYPE = np.dtype([("aabb_hit", np.uint8, 9), ("sat_hit", np.uint8, 9),
                         ("n_contacts", np.uint8, 9), ("pad", np.uint8, 5),
-                        ("normal", np.float32, (9, 2)), ("depth", np.float32, 9)])
-assert TRACE_DTYPE.itemsize == C.sizeof(PairTrace) == 140
+                        ("normal", np.float32, (9, 2)), ("depth", np.float32, 9),
+                        ("contact", np.float32, (9, 2, 2)), ("impulse", np.float32, (9, 2)),
+                        ("joint_depth", np.float32, 4), ("joint_impulse", np.float32, 4)])
+assert TRACE_DTYPE.itemsize == C.sizeof(PairTrace) == 140 + 144 + 72 + 32
 
 
 class BodyView(C.Structure):

@@ -30,7 +30,7 @@ def test_library_exports_every_symbol(wk):
 
 
 def test_struct_layouts(wk):
-    assert C.sizeof(wk.PairTrace) == 140
+    assert C.sizeof(wk.PairTrace) == 388
     assert C.sizeof(wk.BodyView) == 4 + 48 + 8 + 8 + 4 + 4 + 4 + 4
     lib = wk.load_library()
     cfg = wk.default_config()
