@@ -97,12 +97,12 @@ struct ProfScope {
   ProfScope(wk_ctx* c_, int k, int64_t u = 0) : c(c_), kind(k), units(u) {
     if (c->prof) {
       a = ev_get(c); b = ev_get(c);
-      if (a) hipEventRecord(a, c->stream);
+      if (a) (void)hipEventRecord(a, c->stream);
     }
   }
   ~ProfScope() {
     if (c->prof && a && b) {
-      hipEventRecord(b, c->stream);
+      (void)hipEventRecord(b, c->stream);
       c->pending.push_back({kind, a, b, units});
     }
   }
@@ -124,7 +124,7 @@ static void prof_drain(wk_ctx* c) {
 
 static int ensure(wk_ctx* c, void** p, size_t* have, size_t need) {
   if (*have >= need) return 0;
-  if (*p) hipFree(*p);
+  if (*p) (void)hipFree(*p);
   *p = nullptr;
   *have = 0;
   HIPCHK(c, hipMalloc(p, need));
@@ -302,15 +302,15 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
 
 int wk_destroy(wk_ctx* c) {
   if (!c) return WK_OK;
-  if (c->stream) hipStreamSynchronize(c->stream);
-  for (auto& e : c->pending) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
-  for (auto e : c->pool) hipEventDestroy(e);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& e : c->pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+  for (auto e : c->pool) (void)hipEventDestroy(e);
   if (c->comm) ncclCommDestroy(c->comm);
   void* bufs[] = {c->st, c->dxoff, c->mat, c->rng_t, c->W, c->m, c->v, c->grad, c->ts, c->ta,
                   c->tlp, c->tr, c->tv, c->tret, c->tadv, c->td, c->partial, c->scratch, c->scratch2};
   for (void* p : bufs)
-    if (p) hipFree(p);
-  if (c->stream) hipStreamDestroy(c->stream);
+    if (p) (void)hipFree(p);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return WK_OK;
 }
@@ -628,9 +628,10 @@ int wk_set_trajectory(wk_ctx* c, int horizon, const float* s, const float* a, co
 static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   const int per_block = wpb * g.spw;
   const int nblocks = (g.samples + per_block - 1) / per_block;
-  const size_t need = (size_t)nblocks * wk::SLAB;
+  // block slabs followed by the stage-1 group sums of the ordered reduction
+  const size_t need = ((size_t)nblocks + wk::grad_reduce_groups(nblocks)) * wk::SLAB;
   if (c->partial_floats < need) {
-    if (c->partial) hipFree(c->partial);
+    if (c->partial) (void)hipFree(c->partial);
     c->partial = nullptr;
     c->partial_floats = 0;
     HIPCHK(c, hipMalloc((void**)&c->partial, sizeof(float) * need));
@@ -643,7 +644,8 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   }
   {
     ProfScope ps(c, PK_REDUCE);
-    HIPCHK(c, wk::launch_grad_reduce(c->partial, nblocks, c->grad, c->stream));
+    HIPCHK(c, wk::launch_grad_reduce(c->partial, nblocks, c->partial + (size_t)nblocks * wk::SLAB,
+                                     c->grad, c->stream));
   }
   if (c->comm && c->nranks > 1) {
     ProfScope ps(c, PK_ALLRED);

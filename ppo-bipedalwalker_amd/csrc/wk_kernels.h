@@ -79,7 +79,9 @@ hipError_t launch_policy(const EnvParams& P, const float* W, float lp_const, int
 hipError_t launch_returns(int n, int T, int use_gae, float gamma, float lambda, const float* r,
                           const float* v, const uint8_t* d, float* ret, float* adv, hipStream_t s);
 hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t s);
-hipError_t launch_grad_reduce(const float* partial, int nblocks, float* grad, hipStream_t s);
+hipError_t launch_grad_reduce(const float* partial, int nblocks, float* part2, float* grad,
+                              hipStream_t s);
+int grad_reduce_groups(int nblocks);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t s);
 hipError_t launch_normalize(float* x, int n, float eps, hipStream_t s);
 hipError_t launch_xavier(float* W, uint64_t seed, hipStream_t s);

@@ -133,17 +133,18 @@ __global__ __launch_bounds__(64 * WPB) void k_ppo_grad(GradArgs g) {
     h2s[lane] = h2;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // ---- critic output (all lanes, sequential over k) ----
-    float V = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 64; k++) V = V + wl[L_CW2 + k] * hc1s[k];
-    V = V + cb2;
-    // ---- actor output: lanes 0..3 own one action dimension each ----
+    // ---- output layers, one row per lane: lanes 0..3 the actor's 4 outputs (W3 row d
+    // on h2), lane 4 the critic's single output (Wc2 on hc1); sequential over k ----
     const int d = lane & 3;
-    float z3 = 0.0f;
+    const bool vlane = lane == 4;
+    const float* wrow = vlane ? (wl + L_CW2) : (wl + L_AW3 + d * 65);
+    const float* xin = vlane ? hc1s : h2s;
+    float zo = 0.0f;
 #pragma unroll
-    for (int k = 0; k < 64; k++) z3 = z3 + wl[L_AW3 + d * 65 + k] * h2s[k];
-    z3 = z3 + wl[L_AB3 + d];
+    for (int k = 0; k < 64; k++) zo = zo + wrow[k] * xin[k];
+    zo = zo + (vlane ? cb2 : wl[L_AB3 + d]);
+    const float V = __shfl(zo, 4);
+    const float z3 = zo;
     const float mean = tanhf(z3);
     // ---- PPO derivative (PPOAgent.cs:234-326), per dimension ----
     const float A = smp[21];
@@ -250,12 +251,30 @@ __global__ __launch_bounds__(64 * WPB) void k_ppo_grad(GradArgs g) {
   for (int i = threadIdx.x; i < SLAB; i += 64 * WPB) out[i] = slab[i];
 }
 
-// sum block slabs in block order: grad[p] = ((0 + P0[p]) + P1[p]) + ...
-__global__ void k_grad_reduce(const float* __restrict__ partial, int nblocks, float* grad) {
+// Deterministic two-level sum of the block slabs (fixed association, no atomics):
+// stage 1 folds groups of RG consecutive slabs (all RG loads issued before the ordered
+// adds, so the chain is one memory latency, not RG); stage 2 folds the groups in order.
+enum { RG = 16 };
+__global__ void k_grad_reduce1(const float* __restrict__ partial, int nblocks, float* part2) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int g = blockIdx.y;
+  if (p >= SLAB) return;
+  const int b0 = g * RG;
+  float v[RG];
+#pragma unroll
+  for (int j = 0; j < RG; j++) v[j] = (b0 + j < nblocks) ? partial[(size_t)(b0 + j) * SLAB + p] : 0.0f;
+  float acc = 0.0f;
+#pragma unroll
+  for (int j = 0; j < RG; j++)
+    if (b0 + j < nblocks) acc = acc + v[j];
+  part2[(size_t)g * SLAB + p] = acc;
+}
+
+__global__ void k_grad_reduce2(const float* __restrict__ part2, int ngroups, float* grad) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= SLAB) return;
   float acc = 0.0f;
-  for (int b = 0; b < nblocks; b++) acc = acc + partial[(size_t)b * SLAB + p];
+  for (int g = 0; g < ngroups; g++) acc = acc + part2[(size_t)g * SLAB + p];
   grad[p] = acc;
 }
 
@@ -339,8 +358,8 @@ hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t 
   const size_t lds = sizeof(float) * (L_WEND + SLAB + wpb * (64 * 4 + 24));
   static bool attr_set = false;
   if (!attr_set) {  // > 64 KiB of dynamic LDS (gfx950 CU has 160 KiB)
-    hipFuncSetAttribute((const void*)k_ppo_grad<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)k_ppo_grad<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_ppo_grad<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_ppo_grad<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   if (wpb == 1) {
@@ -350,10 +369,15 @@ hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t 
   }
   return hipGetLastError();
 }
-hipError_t launch_grad_reduce(const float* partial, int nblocks, float* grad, hipStream_t s) {
-  hipLaunchKernelGGL(k_grad_reduce, dim3((SLAB + 255) / 256), dim3(256), 0, s, partial, nblocks, grad);
+hipError_t launch_grad_reduce(const float* partial, int nblocks, float* part2, float* grad,
+                              hipStream_t s) {
+  const int ng = (nblocks + RG - 1) / RG;
+  hipLaunchKernelGGL(k_grad_reduce1, dim3((SLAB + 255) / 256, ng), dim3(256), 0, s, partial,
+                     nblocks, part2);
+  hipLaunchKernelGGL(k_grad_reduce2, dim3((SLAB + 255) / 256), dim3(256), 0, s, part2, ng, grad);
   return hipGetLastError();
 }
+int grad_reduce_groups(int nblocks) { return (nblocks + RG - 1) / RG; }
 hipError_t launch_adam(const AdamArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_adam, dim3((NPARAM + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();

@@ -1,0 +1,40 @@
+// Drives the C++ host mirror (csrc/host/nea.hpp) the way the reference's Game1.Update
+// drives Environment.Update, and prints per-step rewards/dones and the final state so
+// tests/test_gpu_parity.py can compare them with the oracle.
+//   test_nea <n_walkers> <steps> <mode: actions|policy>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../ppo-bipedalwalker_amd/csrc/host/nea.hpp"
+
+int main(int argc, char** argv) {
+  int n = argc > 1 ? atoi(argv[1]) : 8;
+  int steps = argc > 2 ? atoi(argv[2]) : 5;
+  bool policy = argc > 3 && strcmp(argv[3], "policy") == 0;
+  NEA::Walker::PPO::Hyperparameters h;
+  NEA::Materials::Carpet carpet;
+  NEA::Environment env(n, h, 20250905, 0, &carpet);
+  const float dt = h.c.DeltaTime;
+  for (int t = 0; t < steps; t++) {
+    if (!policy) {
+      for (int i = 0; i < n; i++) {
+        std::vector<float> a(4);
+        for (int j = 0; j < 4; j++) a[j] = 0.37f * (float)((i + 3 * t + j) % 7) - 1.1f;
+        env.GetWalker(i).TakeActions(a);
+      }
+    }
+    env.Update(dt);
+    for (int i = 0; i < n; i++) printf("R %d %d %.9g %d\n", t, i, env.Rewards()[i], (int)env.Dones()[i]);
+  }
+  for (int i = 0; i < n; i++) {
+    auto s = env.GetWalker(i).GetState();
+    printf("S %d", i);
+    for (float v : s) printf(" %.9g", v);
+    printf("\n");
+  }
+  auto pos = env.GetWalker(0).GetPosition();
+  printf("P %.9g %.9g\n", pos.first, pos.second);
+  return 0;
+}

@@ -1,0 +1,50 @@
+"""The C++ host mirror (csrc/host/nea.hpp: NEA::Environment / Walker / PPOAgent with the
+reference's names) compiles against the C ABI; on a GPU it reproduces the oracle."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "ppo-bipedalwalker_amd")
+
+
+def build_mirror(tmp_path, wk):
+    exe = str(tmp_path / "test_nea")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-o", exe,
+                    os.path.join(ROOT, "tests", "cpp", "test_nea.cpp"), f"-L{PKG}", "-lwk",
+                    f"-Wl,-rpath,{PKG}"], check=True)
+    return exe
+
+
+def test_mirror_compiles_and_fails_loudly_without_gpu(tmp_path, wk):
+    exe = build_mirror(tmp_path, wk)
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu test")
+    r = subprocess.run([exe, "2", "1"], capture_output=True, text=True)
+    assert r.returncode != 0 and "wk_create" in r.stderr
+
+
+@pytest.mark.gpu
+def test_mirror_matches_oracle(tmp_path, wk, orc):
+    exe = build_mirror(tmp_path, wk)
+    n, steps = 8, 30
+    out = subprocess.run([exe, str(n), str(steps), "actions"], capture_output=True, text=True,
+                         check=True, timeout=120).stdout.splitlines()
+    envs = [orc.Env() for _ in range(n)]
+    rew = {}
+    for line in out:
+        if line.startswith("R "):
+            _, t, i, r, d = line.split()
+            rew[(int(t), int(i))] = (np.float32(r), int(d))
+    for t in range(steps):
+        for i, e in enumerate(envs):
+            # 0.37f * (float)((i + 3t + j) % 7) - 1.1f, in fp32 like the C++ driver
+            a = (np.float32(0.37) * np.float32((i + 3 * t + np.arange(4)) % 7) - np.float32(1.1)).astype(np.float32)
+            _, r, d = e.step(a)
+            assert rew[(t, i)] == (np.float32(r), d)
+    states = {int(l.split()[1]): np.array(l.split()[2:], np.float32) for l in out if l.startswith("S ")}
+    for i, e in enumerate(envs):
+        np.testing.assert_array_equal(states[i], e.obs())
