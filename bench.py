@@ -40,6 +40,7 @@ def parse():
     p.add_argument("--minibatch", type=int, default=0, help="per-GPU minibatch (0 = walkers)")
     p.add_argument("--materials", action="store_true", help="config 5: random Ice/Rubber/Carpet")
     p.add_argument("--seed", type=int, default=20250905)
+    p.add_argument("--lanes", type=int, default=16, help="lanes per walker in the physics kernel (1 or 16)")
     p.add_argument("--cpu-baseline-steps", type=int, default=150000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_physics.json"))
@@ -80,7 +81,7 @@ def main():
     eng = wk.Engine(shard.n_local, seed=args.seed, device=local, Horizon=args.horizon,
                     Minibatch=shard.minibatch_local, MinibatchGlobal=shard.minibatch_global,
                     Epochs=args.epochs, EnvOffset=shard.env_offset, RandomizeStart=1,
-                    RandomizeMaterial=1 if args.materials else 0)
+                    RandomizeMaterial=1 if args.materials else 0, LanesPerWalker=args.lanes)
     if world > 1:
         uid = wk.Engine.comm_unique_id() if rank == 0 else None
         uid = broadcast_unique_id(uid)

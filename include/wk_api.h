@@ -102,6 +102,8 @@ typedef struct wk_config {
   int EnvOffset;            /* global id of this context's env 0 (Philox streams) */
   int RandomizeStart;       /* 1: env e starts at x + 200*u_e (BASELINE config 2) */
   int RandomizeMaterial;    /* 1: env material in {Ice, Rubber, Carpet} (config 5) */
+  int LanesPerWalker;       /* physics kernel mapping: 0/16 = SAT axes over a 16-lane row,
+                               1 = one walker per lane (both bit-exact) */
 } wk_config;
 
 /* canonical per-env state dump: WK_STATE_FLOATS floats per env (identical layout to

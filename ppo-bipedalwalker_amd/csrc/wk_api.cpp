@@ -247,6 +247,7 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   P.std_ = expf(c.LogStandardDeviation);
   P.seed = seed;
   P.env_offset = c.EnvOffset;
+  P.lanes = c.LanesPerWalker == 1 ? 1 : 16;
   const float PI_F = 3.14159265358979323846f;
   x->lp_const = -logf(P.std_) - logf(sqrtf(2.0f * PI_F));
 
@@ -426,23 +427,19 @@ int wk_get_obs(wk_ctx* c, float* obs) {
   return WK_OK;
 }
 
+// the device state is [n_env][WK_STATE_FLOATS] (one 448-B record per walker), the same
+// layout as the canonical dump, so these are plain copies
 int wk_get_state(wk_ctx* c, float* state) {
   if (!c || !state) return WK_ERR_ARG;
-  std::vector<float> soa((size_t)wk::NSTATE * c->n);
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpy(soa.data(), c->st, sizeof(float) * soa.size(), hipMemcpyDeviceToHost));
-  for (int e = 0; e < c->n; e++)
-    for (int f = 0; f < wk::NSTATE; f++) state[(size_t)e * wk::NSTATE + f] = soa[(size_t)f * c->n + e];
+  HIPCHK(c, hipMemcpy(state, c->st, sizeof(float) * wk::NSTATE * c->n, hipMemcpyDeviceToHost));
   return WK_OK;
 }
 
 int wk_set_state(wk_ctx* c, const float* state) {
   if (!c || !state) return WK_ERR_ARG;
-  std::vector<float> soa((size_t)wk::NSTATE * c->n);
-  for (int e = 0; e < c->n; e++)
-    for (int f = 0; f < wk::NSTATE; f++) soa[(size_t)f * c->n + e] = state[(size_t)e * wk::NSTATE + f];
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpy(c->st, soa.data(), sizeof(float) * soa.size(), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->st, state, sizeof(float) * wk::NSTATE * c->n, hipMemcpyHostToDevice));
   return WK_OK;
 }
 
@@ -459,8 +456,8 @@ int wk_get_body_view(wk_ctx* c, int env, int body, wk_body_view* o) {
   }
   float f[wk::BSTRIDE];
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  for (int i = 0; i < wk::BSTRIDE; i++)
-    HIPCHK(c, hipMemcpy(&f[i], c->st + (size_t)(body * wk::BSTRIDE + i) * c->n + env, sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(f, c->st + (size_t)env * wk::NSTATE + (size_t)body * wk::BSTRIDE,
+                      sizeof(f), hipMemcpyDeviceToHost));
   o->n_vertices = body == wk::BODY ? 5 : 6;
   for (int i = 0; i < o->n_vertices; i++) { o->vertices[i][0] = f[2 * i]; o->vertices[i][1] = f[2 * i + 1]; }
   o->centroid[0] = f[wk::F_CX]; o->centroid[1] = f[wk::F_CY];

@@ -184,6 +184,95 @@ DEV bool sat(const Poly<NA>& A, const Poly<NB>& B, V2& normal, float& depth) {
   return result;
 }
 
+// ---------------- SAT, axes split over an L-lane row (L in {4, 8, 16}) ----------------
+// Lane `sub` of the walker's row owns axis `sub` (A's edges first, then B's, the order
+// of AxisChecks(A, B) && AxisChecks(B, A)).  The sequential loop's result is exactly:
+// false if any axis separates; otherwise the smallest depth, ties to the lowest axis
+// index (strict '<' in AxisChecks keeps the first).  That is an order-independent
+// lexicographic min over (depth, index), reduced across the row with DPP.
+DEV int dpp_i(int v, int ctrl_sel) {
+  switch (ctrl_sel) {
+    case 0: return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    case 1: return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    case 2: return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    default: return __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false); // row_mirror
+  }
+}
+DEV float dpp_f(float v, int c) { return __int_as_float(dpp_i(__float_as_int(v), c)); }
+
+template <int L>
+DEV void row_reduce(int& sep, float& depth, int& idx, float& nx, float& ny) {
+  constexpr int steps = L == 16 ? 4 : (L == 8 ? 3 : 2);
+#pragma unroll
+  for (int s = 0; s < steps; s++) {
+    const int osep = dpp_i(sep, s), oidx = dpp_i(idx, s);
+    const float od = dpp_f(depth, s), onx = dpp_f(nx, s), ony = dpp_f(ny, s);
+    sep |= osep;
+    const bool take = (od < depth) || (od == depth && oidx < idx);
+    depth = take ? od : depth;
+    idx = take ? oidx : idx;
+    nx = take ? onx : nx;
+    ny = take ? ony : ny;
+  }
+}
+
+// candidate edge endpoints of axis k: A's edges 0..NA-1 then B's edges
+template <int NA, int NB>
+DEV void edge_of(const Poly<NA>& A, const Poly<NB>& B, int k, V2& p0, V2& p1) {
+  uint32_t x0 = 0u, y0 = 0u, x1 = 0u, y1 = 0u;
+#pragma unroll
+  for (int i = 0; i < NA + NB; i++) {
+    const uint32_t m = (k == i) ? 0xffffffffu : 0u;
+    const bool fa = i < NA;
+    const int a = fa ? i : i - NA;
+    const int b = fa ? (a + 1) % NA : (a + 1) % NB;
+    const float sx = fa ? A.x[fa ? a : 0] : B.x[fa ? 0 : a];
+    const float sy = fa ? A.y[fa ? a : 0] : B.y[fa ? 0 : a];
+    const float ex = fa ? A.x[fa ? b : 0] : B.x[fa ? 0 : b];
+    const float ey = fa ? A.y[fa ? b : 0] : B.y[fa ? 0 : b];
+    x0 |= m & __float_as_uint(sx); y0 |= m & __float_as_uint(sy);
+    x1 |= m & __float_as_uint(ex); y1 |= m & __float_as_uint(ey);
+  }
+  p0 = mk(__uint_as_float(x0), __uint_as_float(y0));
+  p1 = mk(__uint_as_float(x1), __uint_as_float(y1));
+}
+
+template <int L, int NA, int NB>
+DEV bool sat_row(const Poly<NA>& A, const Poly<NB>& B, int sub, V2& normal, float& depth) {
+  static_assert(NA + NB <= L, "one axis per lane");
+  int sep = 0, idx = 1 << 20;
+  float d = FLT_MAX, nx = 0.0f, ny = 0.0f;
+  if (sub < NA + NB) {
+    V2 p0, p1;
+    edge_of(A, B, sub, p0, p1);
+    const float ex = p1.x - p0.x, ey = p1.y - p0.y;
+    V2 axis = mk(-ey, ex);
+    if (!(axis.x == 0.0f && axis.y == 0.0f)) {
+      axis = vnormalize(axis);
+      float amin, amax, bmin, bmax;
+      project2(axis.x, axis.y, A, B, amin, amax, bmin, bmax);
+      float temp;
+      bool overlapping;
+      if (sub < NA) {  // AxisChecks(A, B): projectionA = A
+        temp = net_minf(bmax - amin, amax - bmin);
+        overlapping = (amin < bmax) && (bmin < amax);
+      } else {         // AxisChecks(B, A): projectionA = B
+        temp = net_minf(amax - bmin, bmax - amin);
+        overlapping = (bmin < amax) && (amin < bmax);
+      }
+      if (!overlapping) sep = 1;
+      d = temp; idx = sub; nx = axis.x; ny = axis.y;
+    }
+  }
+  row_reduce<L>(sep, d, idx, nx, ny);
+  normal = idx < (1 << 20) ? mk(nx, ny) : mk(0.0f, 0.0f);
+  depth = d;
+  const bool result = sep == 0;
+  V2 dir = mk(B.cx - A.cx, B.cy - A.cy);
+  if (vdot(dir, normal) > 0.0f) normal = vmul(normal, -1.0f);
+  return result;
+}
+
 // ---------------- contact points (ContactPoints.cs:13-134) ----------------
 // Runtime vertex select as a bit-mask OR over compile-time registers.  (A compare/select
 // chain gets folded by LLVM into a load through a selected address, which pins the

@@ -19,6 +19,15 @@
 #include "wk_device.h"
 #include "wk_kernels.h"
 
+#ifndef WK_ENV_WAVES
+#define WK_ENV_WAVES 2
+#endif
+#if WK_ENV_WAVES > 1
+#define WK_ENV_WPE __attribute__((amdgpu_waves_per_eu(WK_ENV_WAVES, WK_ENV_WAVES)))
+#else
+#define WK_ENV_WPE
+#endif
+
 namespace wk {
 
 struct EnvState {
@@ -75,35 +84,35 @@ template <int N>
 DEV void load_poly(Poly<N>& p, const float* __restrict__ st, int b, int e, int n) {
 #pragma unroll
   for (int i = 0; i < N; i++) {
-    p.x[i] = st[(b * BSTRIDE + 2 * i) * n + e];
-    p.y[i] = st[(b * BSTRIDE + 2 * i + 1) * n + e];
+    p.x[i] = st[(size_t)e * NSTATE + (b * BSTRIDE + 2 * i)];
+    p.y[i] = st[(size_t)e * NSTATE + (b * BSTRIDE + 2 * i + 1)];
   }
-  p.cx = st[(b * BSTRIDE + F_CX) * n + e];
-  p.cy = st[(b * BSTRIDE + F_CY) * n + e];
+  p.cx = st[(size_t)e * NSTATE + (b * BSTRIDE + F_CX)];
+  p.cy = st[(size_t)e * NSTATE + (b * BSTRIDE + F_CY)];
 }
 DEV void load_dyn(Dyn& d, bool& col, const float* __restrict__ st, int b, int e, int n) {
-  d.vx = st[(b * BSTRIDE + F_VX) * n + e];
-  d.vy = st[(b * BSTRIDE + F_VY) * n + e];
-  d.w = st[(b * BSTRIDE + F_W) * n + e];
-  d.th = st[(b * BSTRIDE + F_TH) * n + e];
-  col = st[(b * BSTRIDE + F_COL) * n + e] != 0.0f;
+  d.vx = st[(size_t)e * NSTATE + (b * BSTRIDE + F_VX)];
+  d.vy = st[(size_t)e * NSTATE + (b * BSTRIDE + F_VY)];
+  d.w = st[(size_t)e * NSTATE + (b * BSTRIDE + F_W)];
+  d.th = st[(size_t)e * NSTATE + (b * BSTRIDE + F_TH)];
+  col = st[(size_t)e * NSTATE + (b * BSTRIDE + F_COL)] != 0.0f;
 }
 template <int N>
 DEV void store_body(const Poly<N>& p, const Dyn& d, bool col, float* __restrict__ st, int b, int e,
                     int n) {
 #pragma unroll
   for (int i = 0; i < 6; i++) {
-    st[(b * BSTRIDE + 2 * i) * n + e] = i < N ? p.x[i < N ? i : 0] : 0.0f;
-    st[(b * BSTRIDE + 2 * i + 1) * n + e] = i < N ? p.y[i < N ? i : 0] : 0.0f;
+    st[(size_t)e * NSTATE + (b * BSTRIDE + 2 * i)] = i < N ? p.x[i < N ? i : 0] : 0.0f;
+    st[(size_t)e * NSTATE + (b * BSTRIDE + 2 * i + 1)] = i < N ? p.y[i < N ? i : 0] : 0.0f;
   }
-  st[(b * BSTRIDE + F_CX) * n + e] = p.cx;
-  st[(b * BSTRIDE + F_CY) * n + e] = p.cy;
-  st[(b * BSTRIDE + F_VX) * n + e] = d.vx;
-  st[(b * BSTRIDE + F_VY) * n + e] = d.vy;
-  st[(b * BSTRIDE + F_W) * n + e] = d.w;
-  st[(b * BSTRIDE + F_TH) * n + e] = d.th;
-  st[(b * BSTRIDE + F_COL) * n + e] = col ? 1.0f : 0.0f;
-  st[(b * BSTRIDE + 19) * n + e] = 0.0f;
+  st[(size_t)e * NSTATE + (b * BSTRIDE + F_CX)] = p.cx;
+  st[(size_t)e * NSTATE + (b * BSTRIDE + F_CY)] = p.cy;
+  st[(size_t)e * NSTATE + (b * BSTRIDE + F_VX)] = d.vx;
+  st[(size_t)e * NSTATE + (b * BSTRIDE + F_VY)] = d.vy;
+  st[(size_t)e * NSTATE + (b * BSTRIDE + F_W)] = d.w;
+  st[(size_t)e * NSTATE + (b * BSTRIDE + F_TH)] = d.th;
+  st[(size_t)e * NSTATE + (b * BSTRIDE + F_COL)] = col ? 1.0f : 0.0f;
+  st[(size_t)e * NSTATE + (b * BSTRIDE + 19)] = 0.0f;
 }
 
 DEV void load_state(EnvState& s, const float* __restrict__ st, int e, int n) {
@@ -118,15 +127,15 @@ DEV void load_state(EnvState& s, const float* __restrict__ st, int e, int n) {
   load_dyn(s.drll, s.crll, st, RLL, e, n);
   load_dyn(s.drlu, s.crlu, st, RLU, e, n);
 #pragma unroll
-  for (int j = 0; j < 4; j++) s.torque[j] = st[(S_TORQUE + j) * n + e];
-  s.posx = st[S_POS * n + e];
-  s.posy = st[(S_POS + 1) * n + e];
-  s.prevx = st[S_PREV * n + e];
-  s.prevy = st[(S_PREV + 1) * n + e];
-  s.steps = (int)st[S_STEPS * n + e];
-  s.post = st[S_POSTRESET * n + e] != 0.0f;
-  s.terminal = st[S_TERMINAL * n + e] != 0.0f;
-  s.episodes = (int)st[S_EPISODES * n + e];
+  for (int j = 0; j < 4; j++) s.torque[j] = st[(size_t)e * NSTATE + (S_TORQUE + j)];
+  s.posx = st[(size_t)e * NSTATE + S_POS];
+  s.posy = st[(size_t)e * NSTATE + (S_POS + 1)];
+  s.prevx = st[(size_t)e * NSTATE + S_PREV];
+  s.prevy = st[(size_t)e * NSTATE + (S_PREV + 1)];
+  s.steps = (int)st[(size_t)e * NSTATE + S_STEPS];
+  s.post = st[(size_t)e * NSTATE + S_POSTRESET] != 0.0f;
+  s.terminal = st[(size_t)e * NSTATE + S_TERMINAL] != 0.0f;
+  s.episodes = (int)st[(size_t)e * NSTATE + S_EPISODES];
 }
 
 DEV void store_state(const EnvState& s, float* __restrict__ st, int e, int n) {
@@ -136,15 +145,15 @@ DEV void store_state(const EnvState& s, float* __restrict__ st, int e, int n) {
   store_body(s.rll, s.drll, s.crll, st, RLL, e, n);
   store_body(s.rlu, s.drlu, s.crlu, st, RLU, e, n);
 #pragma unroll
-  for (int j = 0; j < 4; j++) st[(S_TORQUE + j) * n + e] = s.torque[j];
-  st[S_POS * n + e] = s.posx;
-  st[(S_POS + 1) * n + e] = s.posy;
-  st[S_PREV * n + e] = s.prevx;
-  st[(S_PREV + 1) * n + e] = s.prevy;
-  st[S_STEPS * n + e] = (float)s.steps;
-  st[S_POSTRESET * n + e] = s.post ? 1.0f : 0.0f;
-  st[S_TERMINAL * n + e] = s.terminal ? 1.0f : 0.0f;
-  st[S_EPISODES * n + e] = (float)s.episodes;
+  for (int j = 0; j < 4; j++) st[(size_t)e * NSTATE + (S_TORQUE + j)] = s.torque[j];
+  st[(size_t)e * NSTATE + S_POS] = s.posx;
+  st[(size_t)e * NSTATE + (S_POS + 1)] = s.posy;
+  st[(size_t)e * NSTATE + S_PREV] = s.prevx;
+  st[(size_t)e * NSTATE + (S_PREV + 1)] = s.prevy;
+  st[(size_t)e * NSTATE + S_STEPS] = (float)s.steps;
+  st[(size_t)e * NSTATE + S_POSTRESET] = s.post ? 1.0f : 0.0f;
+  st[(size_t)e * NSTATE + S_TERMINAL] = s.terminal ? 1.0f : 0.0f;
+  st[(size_t)e * NSTATE + S_EPISODES] = (float)s.episodes;
 }
 
 // Walker.GetState (Walker.cs:132-152)
@@ -165,18 +174,21 @@ DEV void get_obs(const EnvState& s, float o[12]) {
 
 // RigidBody.ResolveCollisions body for one (this=A, other=B) candidate
 // (Bodies/RigidBody.cs:66-96); B may be the static floor.
-template <int NA, int NB, bool BSTATIC, bool TRACE>
+template <int NA, int NB, bool BSTATIC, bool TRACE, int L>
 DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB,
-                      bool& colA, PairTraceDev* tr, int pi) {
+                      bool& colA, PairTraceDev* tr, int pi, int sub) {
   if (!aabb_overlap(A, B)) return;
-  if (TRACE) tr->aabb_hit[pi] = 1;
+  if (TRACE && tr) tr->aabb_hit[pi] = 1;
   if (BSTATIC) colA = true;  // body._isFloor -> Collided = true (:75)
   V2 n;
   float depth;
-  if (!sat(A, B, n, depth)) return;
+  bool hit;
+  if constexpr (L > 1) hit = sat_row<L>(A, B, sub, n, depth);
+  else hit = sat(A, B, n, depth);
+  if (!hit) return;
   V2 c0, c1;
   int nc = contact_points(A, B, n, c0, c1);
-  if (TRACE) {
+  if (TRACE && tr) {
     tr->sat_hit[pi] = 1;
     tr->n_contacts[pi] = (uint8_t)nc;
     tr->normal[pi][0] = n.x;
@@ -203,7 +215,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   float j = calc_impulse(bA, bB, contact, 1.0f + e, n, rA, rB);
   V2 tangent = mk(-n.y, n.x);
   float jf = calc_impulse(bA, bB, contact, mu, tangent, rAF, rBF);
-  if (TRACE) { tr->impulse[pi][0] = j; tr->impulse[pi][1] = jf; }
+  if (TRACE && tr) { tr->impulse[pi][0] = j; tr->impulse[pi][1] = jf; }
   apply_impulses<BSTATIC>(bA, bB, n, j, rA, rB);
   apply_impulses<BSTATIC>(bA, bB, tangent, jf, rAF, rBF);
 }
@@ -223,7 +235,7 @@ DEV void joint_step(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, c
   Body bI{A.cx, A.cy, &dA, mA.im, mA.ii};  // manifold.BodyB = joint body A
   V2 rA, rB;
   float j = calc_impulse(bJ, bI, contact, 1.0f + 1.0f, ab, rA, rB);
-  if (TRACE) { tr->joint_depth[ji] = depth; tr->joint_impulse[ji] = j; }
+  if (TRACE && tr) { tr->joint_depth[ji] = depth; tr->joint_impulse[ji] = j; }
   apply_impulses<false>(bJ, bI, ab, j, rA, rB);
 }
 
@@ -239,9 +251,9 @@ DEV void integrate(Poly<N>& P, Dyn& D, float dt, float adx, float ady) {
 }
 
 // one substep of Environment.StepObjects (:130-142)
-template <bool TRACE>
+template <bool TRACE, int L>
 DEV void substep(EnvState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
-                 PairTraceDev* tr) {
+                 PairTraceDev* tr, int sub) {
   Poly<4> fl;
   floor_poly(fl);
   Dyn dfl;
@@ -258,28 +270,28 @@ DEV void substep(EnvState& s, const Mat& mp, const Mat& mb, float dt, float adx,
   integrate(s.lll, s.dlll, dt, adx, ady);
 #pragma unroll 1
   for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE>(s.lll, s.dlll, mp, fl, dfl, mf, s.clll, tr, 1);
-    else resolve_pair<6, 6, false, TRACE>(s.lll, s.dlll, mp, s.llu, s.dllu, mp, s.clll, tr, 0);
+    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, L>(s.lll, s.dlll, mp, fl, dfl, mf, s.clll, tr, 1, sub);
+    else resolve_pair<6, 6, false, TRACE, L>(s.lll, s.dlll, mp, s.llu, s.dllu, mp, s.clll, tr, 0, sub);
   }
   integrate(s.llu, s.dllu, dt, adx, ady);
 #pragma unroll 1
   for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE>(s.llu, s.dllu, mp, fl, dfl, mf, s.cllu, tr, 3);
-    else resolve_pair<6, 6, false, TRACE>(s.llu, s.dllu, mp, s.lll, s.dlll, mp, s.cllu, tr, 2);
+    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, L>(s.llu, s.dllu, mp, fl, dfl, mf, s.cllu, tr, 3, sub);
+    else resolve_pair<6, 6, false, TRACE, L>(s.llu, s.dllu, mp, s.lll, s.dlll, mp, s.cllu, tr, 2, sub);
   }
   integrate(s.body, s.dbody, dt, adx, ady);
-  resolve_pair<5, 4, true, TRACE>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody, tr, 4);
+  resolve_pair<5, 4, true, TRACE, L>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody, tr, 4, sub);
   integrate(s.rll, s.drll, dt, adx, ady);
 #pragma unroll 1
   for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE>(s.rll, s.drll, mp, fl, dfl, mf, s.crll, tr, 6);
-    else resolve_pair<6, 6, false, TRACE>(s.rll, s.drll, mp, s.rlu, s.drlu, mp, s.crll, tr, 5);
+    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, L>(s.rll, s.drll, mp, fl, dfl, mf, s.crll, tr, 6, sub);
+    else resolve_pair<6, 6, false, TRACE, L>(s.rll, s.drll, mp, s.rlu, s.drlu, mp, s.crll, tr, 5, sub);
   }
   integrate(s.rlu, s.drlu, dt, adx, ady);
 #pragma unroll 1
   for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE>(s.rlu, s.drlu, mp, fl, dfl, mf, s.crlu, tr, 8);
-    else resolve_pair<6, 6, false, TRACE>(s.rlu, s.drlu, mp, s.rll, s.drll, mp, s.crlu, tr, 7);
+    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, L>(s.rlu, s.drlu, mp, fl, dfl, mf, s.crlu, tr, 8, sub);
+    else resolve_pair<6, 6, false, TRACE, L>(s.rlu, s.drlu, mp, s.rll, s.drll, mp, s.crlu, tr, 7, sub);
   }
 }
 
@@ -347,6 +359,81 @@ DEV void sample_actions(const EnvParams& P, float lp_const, uint32_t gid, uint32
   }
 }
 
+// Row-parallel policy for L = 16 lanes per walker: lane `sub` owns neurons 4*sub..4*sub+3
+// of every 64-wide layer (each neuron's sum stays sequential in k, so the values are
+// bit-identical to actor_mean / critic_value); activations cross lanes through a
+// 192-float LDS slice per walker.  Lanes 0..3 own one action dimension each (output
+// neuron, Philox draw, log-density), lane 4 the critic output; results are broadcast
+// back to the row.
+DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+DEV void policy_row(const EnvParams& P, const float* __restrict__ W, float lp_const,
+                    uint32_t gid, uint32_t t, const float obs[12], int sub, int row_base,
+                    float* __restrict__ h, bool want_value, float act[4], float logp[4],
+                    float& value) {
+  float* h1 = h;
+  float* h2 = h + 64;
+  float* hc = h + 128;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int j = sub * 4 + q;
+    float za = 0.0f, zc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      za = za + W[OFF_A_W1 + j * 12 + k] * obs[k];
+      zc = zc + W[OFF_C_W1 + j * 12 + k] * obs[k];
+    }
+    za = za + W[OFF_A_B1 + j];
+    zc = zc + W[OFF_C_B1 + j];
+    h1[j] = net_maxf(0.2f * za, za);
+    hc[j] = net_maxf(0.2f * zc, zc);
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int j = sub * 4 + q;
+    float z = 0.0f;
+#pragma unroll 16
+    for (int k = 0; k < 64; k++) z = z + W[OFF_A_W2 + j * 64 + k] * h1[k];
+    z = z + W[OFF_A_B2 + j];
+    h2[j] = net_maxf(0.2f * z, z);
+  }
+  wave_lds_sync();
+  // output neurons: lanes 0..3 actor (W3 row d on h2), lane 4 critic (Wc2 on hc)
+  const int d = sub & 3;
+  const bool vlane = sub == 4;
+  const float* wrow = vlane ? (W + OFF_C_W2) : (W + OFF_A_W3 + d * 64);
+  const float* xin = vlane ? hc : h2;
+  float zo = 0.0f;
+#pragma unroll 16
+  for (int k = 0; k < 64; k++) zo = zo + wrow[k] * xin[k];
+  zo = zo + (vlane ? W[OFF_C_B2] : W[OFF_A_B3 + d]);
+  const float mean = tanhf(zo);
+  // SampleActions for dimension d (PPOAgent.cs:381-398; NormalDistribution.cs:12-32)
+  const float PI_F = 3.14159265358979323846f;
+  U4 o = philox(P.seed, gid, t, (uint32_t)d, ST_ACT);
+  float u1 = next_double_f(o.x, o.y);
+  const float u2 = next_double_f(o.z, o.w);
+  if (u1 == 0.0f) u1 = 1.0f;
+  const float zn = sqrtf(-2.0f * logf(u1)) * sinf(2.0f * PI_F * u2);
+  const float a = mean + (P.std_ * zn);
+  float fraction = (a - mean) / P.std_;
+  fraction *= fraction;
+  fraction /= 2.0f;
+  const float lp = lp_const - fraction;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    act[q] = __shfl(a, row_base + q);
+    logp[q] = __shfl(lp, row_base + q);
+  }
+  value = want_value ? __shfl(zo, row_base + 4) : 0.0f;
+  wave_lds_sync();  // the slice is rewritten by the next env-step
+}
+
 DEV bool state_finite(const EnvState& s) {
   float acc = 0.0f;
 #pragma unroll
@@ -355,11 +442,17 @@ DEV bool state_finite(const EnvState& s) {
   return acc == 0.0f;
 }
 
-template <bool POLICY, bool RECORD, bool TRACE>
-__global__ __launch_bounds__(64) void k_env_step(EnvParams P, StepArgs A) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+// L lanes per walker (a "row"): the Gauss-Seidel chain runs replicated in every lane of
+// the row (bit-identical state), SAT axes are split one per lane (sat_row); lane 0 of
+// the row owns all stores.  L = 1 is the plain one-walker-per-lane mapping.
+template <bool POLICY, bool RECORD, bool TRACE, int L>
+__global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArgs A) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = tid / L, sub = tid % L;
   const int n = P.n_env;
-  if (e >= n) return;
+  if (e >= n) return;  // whole rows exit together
+  const bool leader = sub == 0;
+  __shared__ float pol_lds[(L == 16 && POLICY) ? 4 * 192 : 1];
   EnvState s;
   load_state(s, A.st, e, n);
   const float dx = A.dxoff[e];
@@ -377,20 +470,28 @@ __global__ __launch_bounds__(64) void k_env_step(EnvParams P, StepArgs A) {
     float a[4], lp[4], obs[12];
     if (POLICY) {
       get_obs(s, obs);
-      float mean[4];
-      actor_mean(A.W, obs, mean);
-      sample_actions(P, A.lp_const, gid, t, mean, a, lp);
+      float v = 0.0f;
+      if constexpr (L == 16) {
+        policy_row(P, A.W, A.lp_const, gid, t, obs, sub, threadIdx.x & ~15,
+                   pol_lds + (threadIdx.x >> 4) * 192, RECORD, a, lp, v);
+      } else {
+        float mean[4];
+        actor_mean(A.W, obs, mean);
+        sample_actions(P, A.lp_const, gid, t, mean, a, lp);
+        if (RECORD) v = critic_value(A.W, obs);
+      }
       if (RECORD) {
-        const size_t idx = (size_t)(A.t0 + k) * n + e;
-        float v = critic_value(A.W, obs);
+        if (leader) {
+          const size_t idx = (size_t)(A.t0 + k) * n + e;
 #pragma unroll
-        for (int i = 0; i < 12; i++) A.traj_s[idx * 12 + i] = obs[i];
+          for (int i = 0; i < 12; i++) A.traj_s[idx * 12 + i] = obs[i];
 #pragma unroll
-        for (int d = 0; d < 4; d++) {
-          A.traj_a[idx * 4 + d] = a[d];
-          A.traj_lp[idx * 4 + d] = lp[d];
+          for (int d = 0; d < 4; d++) {
+            A.traj_a[idx * 4 + d] = a[d];
+            A.traj_lp[idx * 4 + d] = lp[d];
+          }
+          A.traj_v[idx] = v;
         }
-        A.traj_v[idx] = v;
       }
     } else {
 #pragma unroll
@@ -413,12 +514,12 @@ __global__ __launch_bounds__(64) void k_env_step(EnvParams P, StepArgs A) {
 #pragma unroll 1
     for (int it = 0; it < P.iterations; it++) {
       PairTraceDev* tr = nullptr;
-      if (TRACE) {
+      if (TRACE && leader) {
         tr = A.trace + ((size_t)e * P.iterations + it);
         PairTraceDev z = {};
         *tr = z;
       }
-      substep<TRACE>(s, mp, mb, dt, adx, ady, tr);
+      substep<TRACE, L>(s, mp, mb, dt, adx, ady, tr, sub);
     }
     // Walker.Update
     s.prevx = s.posx; s.prevy = s.posy;
@@ -446,23 +547,27 @@ __global__ __launch_bounds__(64) void k_env_step(EnvParams P, StepArgs A) {
       s.post = true;
       s.episodes = ep;
     }
-    if (A.obs_out) {
-      get_obs(s, obs);
+    if (leader) {
+      if (A.obs_out) {
+        get_obs(s, obs);
 #pragma unroll
-      for (int i = 0; i < 12; i++) A.obs_out[((size_t)k * n + e) * 12 + i] = obs[i];
-    }
-    if (A.rew_out) A.rew_out[(size_t)k * n + e] = reward;
-    if (A.done_out) A.done_out[(size_t)k * n + e] = terminal ? 1 : 0;
-    if (RECORD) {
-      const size_t idx = (size_t)(A.t0 + k) * n + e;
-      A.traj_r[idx] = reward;
-      A.traj_d[idx] = terminal ? 1 : 0;
+        for (int i = 0; i < 12; i++) A.obs_out[((size_t)k * n + e) * 12 + i] = obs[i];
+      }
+      if (A.rew_out) A.rew_out[(size_t)k * n + e] = reward;
+      if (A.done_out) A.done_out[(size_t)k * n + e] = terminal ? 1 : 0;
+      if (RECORD) {
+        const size_t idx = (size_t)(A.t0 + k) * n + e;
+        A.traj_r[idx] = reward;
+        A.traj_d[idx] = terminal ? 1 : 0;
+      }
     }
     t++;
   }
-  store_state(s, A.st, e, n);
-  A.rng_t[e] = t;
-  if (A.fault_out) A.fault_out[e] |= fault;
+  if (leader) {
+    store_state(s, A.st, e, n);
+    A.rng_t[e] = t;
+    if (A.fault_out) A.fault_out[e] |= fault;
+  }
 }
 
 // env initialisation: Environment ctor (Environment.cs:39-51) -- episode-0 body order
@@ -472,7 +577,7 @@ __global__ void k_env_init(EnvParams P, float* st, const float* dxoff, const uin
   if (e >= P.n_env) return;
   if (mask && !mask[e]) return;
   EnvState s;
-  int episodes = post ? (int)st[S_EPISODES * P.n_env + e] : 0;
+  int episodes = post ? (int)st[(size_t)e * NSTATE + S_EPISODES] : 0;
   make_template(s, dxoff[e]);
   s.post = post != 0;
   s.episodes = episodes;
@@ -544,24 +649,23 @@ __global__ void k_returns(int n, int T, int use_gae, float gamma, float lambda,
   }
 }
 
-// explicit instantiations used by the host
-template __global__ void k_env_step<false, false, false>(EnvParams, StepArgs);
-template __global__ void k_env_step<false, false, true>(EnvParams, StepArgs);
-template __global__ void k_env_step<true, false, false>(EnvParams, StepArgs);
-template __global__ void k_env_step<true, true, false>(EnvParams, StepArgs);
-
 }  // namespace wk
 
 // host-side launch shims (C++ linkage, used by wk_api.cpp)
 namespace wk {
-hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
-  dim3 blk(64), grd((P.n_env + 63) / 64);
+template <int L>
+static void launch_lanes(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
+  dim3 blk(64), grd((unsigned)(((size_t)P.n_env * L + 63) / 64));
   switch (mode) {
-    case 0: hipLaunchKernelGGL((k_env_step<false, false, false>), grd, blk, 0, s, P, A); break;
-    case 1: hipLaunchKernelGGL((k_env_step<false, false, true>), grd, blk, 0, s, P, A); break;
-    case 2: hipLaunchKernelGGL((k_env_step<true, false, false>), grd, blk, 0, s, P, A); break;
-    default: hipLaunchKernelGGL((k_env_step<true, true, false>), grd, blk, 0, s, P, A); break;
+    case 0: hipLaunchKernelGGL((k_env_step<false, false, false, L>), grd, blk, 0, s, P, A); break;
+    case 1: hipLaunchKernelGGL((k_env_step<false, false, true, L>), grd, blk, 0, s, P, A); break;
+    case 2: hipLaunchKernelGGL((k_env_step<true, false, false, L>), grd, blk, 0, s, P, A); break;
+    default: hipLaunchKernelGGL((k_env_step<true, true, false, L>), grd, blk, 0, s, P, A); break;
   }
+}
+hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
+  if (P.lanes == 16) launch_lanes<16>(mode, P, A, s);
+  else launch_lanes<1>(mode, P, A, s);
   return hipGetLastError();
 }
 hipError_t launch_env_init(const EnvParams& P, float* st, const float* dx, const uint8_t* mask,

@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libwk.so")
+# WK_LIB selects an alternative in-tree build (kernel A/B experiments)
+LIB_PATH = os.environ.get("WK_LIB") or os.path.join(os.path.dirname(_HERE), "libwk.so")
 
 STATE_FLOATS = 112
 NPARAM = 6149
@@ -46,6 +47,7 @@ class WkConfig(C.Structure):
         ("ActorNeuralNetwork", C.c_char_p), ("DeltaTime", C.c_float), ("Horizon", C.c_int),
         ("Minibatch", C.c_int), ("MinibatchGlobal", C.c_int), ("EnvOffset", C.c_int),
         ("RandomizeStart", C.c_int), ("RandomizeMaterial", C.c_int),
+        ("LanesPerWalker", C.c_int),
     ]
 
 
