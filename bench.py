@@ -5,8 +5,10 @@ One "step" = one PPO iteration over this rank's walkers: a device-resident rollo
 `--horizon` env-steps (policy sampling + 50 physics substeps + reward/terminal/auto-reset
 + value estimate, fused in one HIP kernel) followed by the returns scan and the PPO
 update (E epochs x pool/M minibatches: gradient kernel -> ordered reduction -> RCCL
-all-reduce -> Adam).  Walkers are sharded weakly: --walkers per GPU (config 4: 8,192 per
-GPU, 65,536 on 8 GPUs).  value = env-steps of all ranks / max-over-ranks wall time.
+all-reduce -> Adam).  The metric's configuration (BASELINE.json: 65,536 walkers) fits one MI355X, so it is the
+N=1 workload; walkers are independent, so N GPUs run weakly scaled shards of --walkers
+each (65,536 per GPU) with only the policy-gradient all-reduce between them.
+value = env-steps of all ranks / max-over-ranks wall time.
 
   python bench.py [--gpus N --steps K --warmup W --walkers 8192 --horizon 64]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -34,13 +36,14 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--walkers", type=int, default=8192, help="walkers per GPU")
+    p.add_argument("--walkers", type=int, default=65536, help="walkers per GPU")
     p.add_argument("--horizon", type=int, default=64)
     p.add_argument("--epochs", type=int, default=5)
     p.add_argument("--minibatch", type=int, default=0, help="per-GPU minibatch (0 = walkers)")
     p.add_argument("--materials", action="store_true", help="config 5: random Ice/Rubber/Carpet")
     p.add_argument("--seed", type=int, default=20250905)
-    p.add_argument("--lanes", type=int, default=16, help="lanes per walker in the physics kernel (1 or 16)")
+    p.add_argument("--lanes", type=int, default=0,
+                   help="lanes per walker in the physics kernel (0 auto, 1, 2 or 16)")
     p.add_argument("--cpu-baseline-steps", type=int, default=150000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_physics.json"))
@@ -152,7 +155,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic (Philox-randomised start offsets; random-init Xavier policy)",
         "config": {
-            "workload": ("BASELINE config 4 per-GPU share (config 3 shape): "
+            "workload": ("BASELINE config 4 walker count (65,536) per GPU, config 3 step: "
                          f"{shard.n_local} walkers/GPU, rollout T_h={args.horizon} with policy "
                          f"sampling + PPO update E={args.epochs}, M={shard.minibatch_local}/GPU"
                          + (", per-env Ice/Rubber/Carpet (config 5)" if args.materials else "")),

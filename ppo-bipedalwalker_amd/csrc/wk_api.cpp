@@ -199,6 +199,9 @@ static int validate(const wk_config* c, std::string& why) {
   }
   if (c->Horizon <= 0) return bad("Horizon must be > 0");
   if (c->Minibatch < 0) return bad("Minibatch must be >= 0");
+  if (c->LanesPerWalker != 0 && c->LanesPerWalker != 1 && c->LanesPerWalker != 2 &&
+      c->LanesPerWalker != 16)
+    return bad("LanesPerWalker must be 0 (auto), 1, 2 or 16");
   return WK_OK;
 }
 
@@ -247,7 +250,9 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   P.std_ = expf(c.LogStandardDeviation);
   P.seed = seed;
   P.env_offset = c.EnvOffset;
-  P.lanes = c.LanesPerWalker == 1 ? 1 : 16;
+  // auto: the side-split pair mapping once it fills every SIMD twice (2 lanes x 32k
+  // walkers = 1024 SIMDs x 2 waves), the 16-lane SAT rows below that
+  P.lanes = c.LanesPerWalker ? c.LanesPerWalker : (n_env >= 32768 ? 2 : 16);
   const float PI_F = 3.14159265358979323846f;
   x->lp_const = -logf(P.std_) - logf(sqrtf(2.0f * PI_F));
 
@@ -411,6 +416,7 @@ int wk_step_traced(wk_ctx* c, const float* actions, wk_pair_trace* trace) {
   float* d_act = (float*)c->scratch2;
   void* d_tr = (char*)c->scratch2 + ((b_act + 63) / 64) * 64;
   HIPCHK(c, hipMemcpyAsync(d_act, actions, b_act, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(d_tr, 0, b_tr, c->stream));
   int r = step_impl(c, d_act, 1, nullptr, nullptr, nullptr, nullptr, 1, d_tr);
   if (r) return r;
   HIPCHK(c, hipMemcpyAsync(trace, d_tr, b_tr, hipMemcpyDeviceToHost, c->stream));

@@ -134,7 +134,7 @@ struct EnvParams {
   float std_;           // MathF.Exp(LogStandardDeviation)
   uint64_t seed;
   int env_offset;
-  int lanes;            // lanes per walker in k_env_step (1 or 16)
+  int lanes;            // lanes per walker in the env-step kernel (1, 2 or 16)
 };
 
 }  // namespace wk

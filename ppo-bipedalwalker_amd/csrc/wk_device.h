@@ -115,13 +115,15 @@ DEV void rotate(Poly<N>& p, float angle) {
 // BoundingBox.FindSignificantCorners + IsColliding (Skeleton.cs:133-176)
 template <int N>
 DEV void aabb(const Poly<N>& p, float& mnx, float& mny, float& mxx, float& mxy) {
+  // IsColliding only compares these, so v_max/v_min (which may pick the other signed
+  // zero of a +0/-0 tie) give the same verdict as the sequential compare-and-replace
   float maxX = -FLT_MAX, maxY = -FLT_MAX, minX = FLT_MAX, minY = FLT_MAX;
 #pragma unroll
   for (int i = 0; i < N; i++) {
-    if (p.x[i] > maxX) maxX = p.x[i];
-    if (p.y[i] > maxY) maxY = p.y[i];
-    if (p.x[i] < minX) minX = p.x[i];
-    if (p.y[i] < minY) minY = p.y[i];
+    maxX = __builtin_fmaxf(maxX, p.x[i]);
+    maxY = __builtin_fmaxf(maxY, p.y[i]);
+    minX = __builtin_fminf(minX, p.x[i]);
+    minY = __builtin_fminf(minY, p.y[i]);
   }
   mnx = minX; mny = minY; mxx = maxX; mxy = maxY;
 }
@@ -137,18 +139,21 @@ DEV bool aabb_overlap(const Poly<NA>& a, const Poly<NB>& b) {
 template <int NA, int NB>
 DEV void project2(float ax, float ay, const Poly<NA>& A, const Poly<NB>& B, float& amin,
                   float& amax, float& bmin, float& bmax) {
+  // min/max by value (v_min/v_max): a +0/-0 tie may keep the other zero than the
+  // sequential compare-and-replace, which cannot change AxisChecks -- an overlapping
+  // axis has bmax - amin > 0 and amax - bmin > 0, so no zero reaches depth.
   amin = FLT_MAX; amax = -FLT_MAX; bmin = FLT_MAX; bmax = -FLT_MAX;
 #pragma unroll
   for (int i = 0; i < NA; i++) {
     float p = ax * A.x[i] + ay * A.y[i];
-    if (p < amin) amin = p;
-    if (p > amax) amax = p;
+    amin = __builtin_fminf(amin, p);
+    amax = __builtin_fmaxf(amax, p);
   }
 #pragma unroll
   for (int i = 0; i < NB; i++) {
     float p = ax * B.x[i] + ay * B.y[i];
-    if (p < bmin) bmin = p;
-    if (p > bmax) bmax = p;
+    bmin = __builtin_fminf(bmin, p);
+    bmax = __builtin_fmaxf(bmax, p);
   }
 }
 

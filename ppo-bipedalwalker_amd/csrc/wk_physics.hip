@@ -570,6 +570,268 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArg
   }
 }
 
+// ---------------- side-split mapping: a lane pair per walker (L = 2) ----------------
+// Lane `side` of the pair (0 = left leg, 1 = right leg) owns that leg's two segments; the
+// torso is held replicated by both.  Inside StepObjects (Environment.cs:130-142) the
+// RigidBody.Step calls run in list order LLL, LLU, BODY, RLL, RLU and every candidate
+// pair is either inside one leg or against the static floor (Walker.cs:212-234), so the
+// left and right collision chains touch disjoint bodies: both run at once, one per lane,
+// and the torso's own step + floor pair runs replicated (bit-identical in both lanes).
+// Joints 0 and 1 (Walker.cs:182-187) both move the torso, so they run one lane at a time
+// with the torso copied across the pair after each; joints 2 and 3 run at once.  Every
+// per-body operation is the same op sequence as the one-lane mapping, so trajectories
+// stay bit-identical to the oracle.
+struct SideState {
+  Poly<6> lo, up;  // this side's lower / upper leg segment
+  Poly<5> body;
+  Dyn dlo, dup, dbody;
+  bool clo, cup, cbody;
+  float tq_up, tq_lo;  // joint torques [side] (body-upper) and [2 + side] (upper-lower)
+  float posx, posy, prevx, prevy;
+  int steps, episodes;
+  bool post, terminal;
+};
+
+template <int CTRL>
+DEV float dppc(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+DEV float pswap(float v) { return dppc<0xB1>(v); }  // quad_perm [1,0,3,2]: the partner lane
+
+// copy the torso from the even (CTRL = quad_perm [0,0,2,2]) or odd ([1,1,3,3]) lane
+template <int CTRL>
+DEV void bcast_torso(Poly<5>& b, Dyn& d) {
+#pragma unroll
+  for (int i = 0; i < 5; i++) { b.x[i] = dppc<CTRL>(b.x[i]); b.y[i] = dppc<CTRL>(b.y[i]); }
+  b.cx = dppc<CTRL>(b.cx); b.cy = dppc<CTRL>(b.cy);
+  d.vx = dppc<CTRL>(d.vx); d.vy = dppc<CTRL>(d.vy); d.w = dppc<CTRL>(d.w);
+}
+
+DEV void load_side(SideState& s, const float* __restrict__ st, int e, int side) {
+  const int blo = side ? RLL : LLL, bup = side ? RLU : LLU;
+  load_poly(s.lo, st, blo, e, 0);
+  load_poly(s.up, st, bup, e, 0);
+  load_poly(s.body, st, BODY, e, 0);
+  load_dyn(s.dlo, s.clo, st, blo, e, 0);
+  load_dyn(s.dup, s.cup, st, bup, e, 0);
+  load_dyn(s.dbody, s.cbody, st, BODY, e, 0);
+  const float* r = st + (size_t)e * NSTATE;
+  s.tq_up = r[S_TORQUE + side];
+  s.tq_lo = r[S_TORQUE + 2 + side];
+  s.posx = r[S_POS]; s.posy = r[S_POS + 1];
+  s.prevx = r[S_PREV]; s.prevy = r[S_PREV + 1];
+  s.steps = (int)r[S_STEPS];
+  s.post = r[S_POSTRESET] != 0.0f;
+  s.terminal = r[S_TERMINAL] != 0.0f;
+  s.episodes = (int)r[S_EPISODES];
+}
+
+DEV void store_side(const SideState& s, float* __restrict__ st, int e, int side) {
+  store_body(s.lo, s.dlo, s.clo, st, side ? RLL : LLL, e, 0);
+  store_body(s.up, s.dup, s.cup, st, side ? RLU : LLU, e, 0);
+  float* r = st + (size_t)e * NSTATE;
+  r[S_TORQUE + side] = s.tq_up;
+  r[S_TORQUE + 2 + side] = s.tq_lo;
+  if (side == 0) {
+    store_body(s.body, s.dbody, s.cbody, st, BODY, e, 0);
+    r[S_POS] = s.posx; r[S_POS + 1] = s.posy;
+    r[S_PREV] = s.prevx; r[S_PREV + 1] = s.prevy;
+    r[S_STEPS] = (float)s.steps;
+    r[S_POSTRESET] = s.post ? 1.0f : 0.0f;
+    r[S_TERMINAL] = s.terminal ? 1.0f : 0.0f;
+    r[S_EPISODES] = (float)s.episodes;
+  }
+}
+
+// Walker.CreateCreature / Reset (both legs are the same two poles) -- cf. make_template
+DEV void make_template_side(SideState& s, float dx) {
+  float px = 125.0f + dx, py = 800.0f;
+  s.body.x[0] = px + 20; s.body.y[0] = py + 20;
+  s.body.x[1] = px;      s.body.y[1] = py + 20;
+  s.body.x[2] = px - 20; s.body.y[2] = py + 20;
+  s.body.x[3] = px - 20; s.body.y[3] = py - 20;
+  s.body.x[4] = px + 20; s.body.y[4] = py - 20;
+  find_centroid(s.body);
+  make_pole(s.up, px + 0.0f, py + 30.0f);
+  make_pole(s.lo, px + 0.0f, py + 60.0f);
+  zero_dyn(s.dlo); zero_dyn(s.dup); zero_dyn(s.dbody);
+  s.clo = s.cup = s.cbody = false;
+  s.tq_up = 0.0f; s.tq_lo = 0.0f;
+  s.steps = 0;
+  s.terminal = false;
+  s.prevx = px; s.prevy = py;
+  s.posx = s.body.cx; s.posy = s.body.cy;
+}
+
+// Walker.GetState (Walker.cs:132-152) assembled from both lanes of the pair
+DEV void get_obs_side(const SideState& s, int side, float o[12]) {
+  const float ux = s.up.x[2], uy = s.up.y[2], tlo = s.dlo.th, tup = s.dup.th;
+  const float oux = pswap(ux), ouy = pswap(uy), otlo = pswap(tlo), otup = pswap(tup);
+  const bool left = side == 0;
+  o[0] = s.body.x[1] / 900.0f;
+  o[1] = s.body.y[1] / 500.0f;
+  o[2] = (left ? ux : oux) / 900.0f;
+  o[3] = (left ? uy : ouy) / 500.0f;
+  o[4] = (left ? oux : ux) / 900.0f;
+  o[5] = (left ? ouy : uy) / 500.0f;
+  o[6] = s.dbody.vx / 60.0f;
+  o[7] = s.dbody.vy / 60.0f;
+  o[8] = left ? tlo : otlo;
+  o[9] = left ? tup : otup;
+  o[10] = left ? otlo : tlo;
+  o[11] = left ? otup : tup;
+}
+
+template <bool TRACE>
+DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
+                      PairTraceDev* tr, int side) {
+  Poly<4> fl;
+  floor_poly(fl);
+  Dyn dfl;
+  zero_dyn(dfl);
+  const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};
+  // joints [bodyJointLeft, bodyJointRight, leftJoint, rightJoint] (Walker.cs:182-187)
+  if (side == 0) joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.up, s.dup, mp, tr, 0);
+  bcast_torso<0xA0>(s.body, s.dbody);
+  if (side == 1) joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.up, s.dup, mp, tr, 1);
+  bcast_torso<0xF5>(s.body, s.dbody);
+  joint_step<6, 6, 2, 3, TRACE>(s.up, s.dup, mp, s.lo, s.dlo, mp, tr, 2 + side);
+  // this leg's RigidBody.Step calls (lower then upper), floor-first after a reset
+  const int pb = side ? 5 : 0;
+  integrate(s.lo, s.dlo, dt, adx, ady);
+#pragma unroll 1
+  for (int q = 0; q < 2; q++) {
+    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1>(s.lo, s.dlo, mp, fl, dfl, mf, s.clo, tr, pb + 1, 0);
+    else resolve_pair<6, 6, false, TRACE, 1>(s.lo, s.dlo, mp, s.up, s.dup, mp, s.clo, tr, pb + 0, 0);
+  }
+  integrate(s.up, s.dup, dt, adx, ady);
+#pragma unroll 1
+  for (int q = 0; q < 2; q++) {
+    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1>(s.up, s.dup, mp, fl, dfl, mf, s.cup, tr, pb + 3, 0);
+    else resolve_pair<6, 6, false, TRACE, 1>(s.up, s.dup, mp, s.lo, s.dlo, mp, s.cup, tr, pb + 2, 0);
+  }
+  // the torso's step, replicated in both lanes (traced by the left lane)
+  integrate(s.body, s.dbody, dt, adx, ady);
+  resolve_pair<5, 4, true, TRACE, 1>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody,
+                                     side == 0 ? tr : nullptr, 4, 0);
+}
+
+DEV bool side_finite(const SideState& s) {
+  float acc = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 6; i++) acc += s.lo.x[i] * 0.0f + s.up.x[i] * 0.0f;
+  acc += s.dbody.vx * 0.0f + s.dbody.vy * 0.0f + s.body.cx * 0.0f + s.body.cy * 0.0f;
+  return acc == 0.0f;
+}
+
+template <bool POLICY, bool RECORD, bool TRACE>
+__global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArgs A) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = tid >> 1, side = tid & 1;
+  const int n = P.n_env;
+  if (e >= n) return;  // both lanes of a pair exit together
+  const bool leader = side == 0;
+  SideState s;
+  load_side(s, A.st, e, side);
+  const float dx = A.dxoff[e];
+  const MatConst mc = material(A.mat[e]);
+  const Mat mp{mc.inv_mass, 0.001f * mc.inv_mass, mc.restitution, mc.friction};
+  const Mat mb{mc.inv_mass, 0.0003f, mc.restitution, mc.friction};  // Walker.cs:168
+  const float dt = P.dt_sub;
+  const float adx = 0.0f * dt, ady = 980.0f * dt;
+  const uint32_t gid = (uint32_t)(P.env_offset + e);
+  uint32_t t = A.rng_t[e];
+  uint32_t fault = 0;
+
+#pragma unroll 1
+  for (int k = 0; k < A.k_steps; k++) {
+    float a[4], lp[4], obs[12];
+    if (POLICY) {
+      get_obs_side(s, side, obs);
+      float mean[4];
+      actor_mean(A.W, obs, mean);
+      sample_actions(P, A.lp_const, gid, t, mean, a, lp);
+      float v = 0.0f;
+      if (RECORD) v = critic_value(A.W, obs);
+      if (RECORD && leader) {
+        const size_t idx = (size_t)(A.t0 + k) * n + e;
+#pragma unroll
+        for (int i = 0; i < 12; i++) A.traj_s[idx * 12 + i] = obs[i];
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+          A.traj_a[idx * 4 + d] = a[d];
+          A.traj_lp[idx * 4 + d] = lp[d];
+        }
+        A.traj_v[idx] = v;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < 4; d++) a[d] = A.actions[((size_t)k * n + e) * 4 + d];
+    }
+    s.steps++;
+    // Clip + Joint.SetTorque: joint `side` drives this upper leg, joint 2+side the lower
+    {
+      const float au = clip1(side ? a[1] : a[0]), al = clip1(side ? a[3] : a[2]);
+      float c = au - s.tq_up; s.tq_up = au; s.dup.w = s.dup.w + c * 5.0f;
+      c = al - s.tq_lo; s.tq_lo = al; s.dlo.w = s.dlo.w + c * 5.0f;
+    }
+#pragma unroll 1
+    for (int it = 0; it < P.iterations; it++) {
+      PairTraceDev* tr = TRACE ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
+      substep_side<TRACE>(s, mp, mb, dt, adx, ady, tr, side);
+    }
+    // Walker.Update + terminal flags (both upper legs and the torso)
+    s.prevx = s.posx; s.prevy = s.posy;
+    s.posx = s.body.cx; s.posy = s.body.cy;
+    const bool other_cup = pswap(s.cup ? 1.0f : 0.0f) != 0.0f;
+    if (s.cbody || s.cup || other_cup) s.terminal = true;
+    float reward = 0.0f;
+    float dX = s.posx - s.prevx;
+    float yb = s.body.y[1];
+    reward = reward + ((dX > 0.0f && ((yb / 500.0f) < 1.6f)) ? dX : 0.0f);
+    reward = reward - (((yb / 500.0f) > 1.65f) ? -0.1f : 0.0f);
+    bool terminal = false;
+    if (s.terminal || s.steps > P.max_timesteps) {
+      if (s.terminal) reward -= 40.0f;
+      terminal = true;
+    }
+    if (s.posx > 900.0f) {
+      reward += 80.0f;
+      terminal = true;
+    }
+    if (!side_finite(s)) fault |= 1u;
+    if (terminal) {
+      int ep = s.episodes + 1;
+      make_template_side(s, dx);
+      s.post = true;
+      s.episodes = ep;
+    }
+    if (A.obs_out) {
+      get_obs_side(s, side, obs);
+      if (leader) {
+#pragma unroll
+        for (int i = 0; i < 12; i++) A.obs_out[((size_t)k * n + e) * 12 + i] = obs[i];
+      }
+    }
+    if (leader) {
+      if (A.rew_out) A.rew_out[(size_t)k * n + e] = reward;
+      if (A.done_out) A.done_out[(size_t)k * n + e] = terminal ? 1 : 0;
+      if (RECORD) {
+        const size_t idx = (size_t)(A.t0 + k) * n + e;
+        A.traj_r[idx] = reward;
+        A.traj_d[idx] = terminal ? 1 : 0;
+      }
+    }
+    t++;
+  }
+  store_side(s, A.st, e, side);
+  fault |= (uint32_t)pswap((float)fault);
+  if (leader) {
+    A.rng_t[e] = t;
+    if (A.fault_out) A.fault_out[e] |= fault;
+  }
+}
+
 // env initialisation: Environment ctor (Environment.cs:39-51) -- episode-0 body order
 __global__ void k_env_init(EnvParams P, float* st, const float* dxoff, const uint8_t* mask,
                            int post) {
@@ -663,8 +925,18 @@ static void launch_lanes(int mode, const EnvParams& P, const StepArgs& A, hipStr
     default: hipLaunchKernelGGL((k_env_step<true, true, false, L>), grd, blk, 0, s, P, A); break;
   }
 }
+static void launch_side(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
+  dim3 blk(64), grd((unsigned)(((size_t)P.n_env * 2 + 63) / 64));
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((k_env_side<false, false, false>), grd, blk, 0, s, P, A); break;
+    case 1: hipLaunchKernelGGL((k_env_side<false, false, true>), grd, blk, 0, s, P, A); break;
+    case 2: hipLaunchKernelGGL((k_env_side<true, false, false>), grd, blk, 0, s, P, A); break;
+    default: hipLaunchKernelGGL((k_env_side<true, true, false>), grd, blk, 0, s, P, A); break;
+  }
+}
 hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
-  if (P.lanes == 16) launch_lanes<16>(mode, P, A, s);
+  if (P.lanes == 2) launch_side(mode, P, A, s);
+  else if (P.lanes == 16) launch_lanes<16>(mode, P, A, s);
   else launch_lanes<1>(mode, P, A, s);
   return hipGetLastError();
 }

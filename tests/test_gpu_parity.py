@@ -15,6 +15,8 @@ pytestmark = pytest.mark.gpu
 
 SEED = 20250905
 F = np.float32
+LANES = [1, 2, 16]  # physics mappings: lane per walker, side-split pair, SAT rows
+lanes_param = pytest.mark.parametrize("lanes", LANES)
 
 
 def oracle_envs(orc, eng, n):
@@ -39,9 +41,10 @@ def test_template_state_bitexact(wk, orc):
     np.testing.assert_array_equal(eng.get_obs(), np.stack([e.obs() for e in envs]))
 
 
-def test_one_step_trace_bitexact(wk, orc):
+@lanes_param
+def test_one_step_trace_bitexact(wk, orc, lanes):
     n = 128
-    eng = wk.Engine(n, seed=SEED, RandomizeStart=1, RandomizeMaterial=1)
+    eng = wk.Engine(n, seed=SEED, RandomizeStart=1, RandomizeMaterial=1, LanesPerWalker=lanes)
     envs, _, _ = oracle_envs(orc, eng, n)
     rng = np.random.default_rng(1)
     acts = rng.uniform(-1.3, 1.3, (n, 4)).astype(F)  # includes clipped values
@@ -50,14 +53,15 @@ def test_one_step_trace_bitexact(wk, orc):
         _, _, _, t = e.step(acts[i], trace=True)
         for k in ("aabb_hit", "sat_hit", "n_contacts"):
             np.testing.assert_array_equal(tr[i][k], t[k], err_msg=f"env {i} {k}")
-        for k in ("normal", "depth"):
+        for k in ("normal", "depth", "contact", "impulse", "joint_depth", "joint_impulse"):
             np.testing.assert_array_equal(tr[i][k], t[k], err_msg=f"env {i} {k}")
     np.testing.assert_array_equal(eng.get_state(), np.stack([e.dump() for e in envs]))
 
 
-def test_golden_one_step(wk, golden):
+@lanes_param
+def test_golden_one_step(wk, golden, lanes):
     g = golden("env_step_trace.npz")
-    eng = wk.Engine(1, seed=SEED)
+    eng = wk.Engine(1, seed=SEED, LanesPerWalker=lanes)
     np.testing.assert_array_equal(eng.get_state()[0], g["state0"])
     tr = eng.step_traced(g["action"][None])[0]
     for k in ("aabb_hit", "sat_hit", "n_contacts", "normal", "depth"):
@@ -65,11 +69,12 @@ def test_golden_one_step(wk, golden):
     np.testing.assert_array_equal(eng.get_state()[0], g["state1"])
 
 
-def test_golden_thousand_steps_bitexact(wk, orc, golden):
+@lanes_param
+def test_golden_thousand_steps_bitexact(wk, orc, golden, lanes):
     """1000 identical env-steps for 8 walkers (auto-resets included): drift must be 0."""
     g = golden("thousand_steps.npz")
     n = g["dx"].size
-    eng = wk.Engine(n, seed=SEED)
+    eng = wk.Engine(n, seed=SEED, LanesPerWalker=lanes)
     eng.set_offsets(g["dx"])
     eng.reset()
     # the fixture starts in episode 0 (floor last): restore that flag after the reset
@@ -85,9 +90,10 @@ def test_golden_thousand_steps_bitexact(wk, orc, golden):
         assert not fault.any()
 
 
-def test_many_envs_multi_step_bitexact(wk, orc):
+@lanes_param
+def test_many_envs_multi_step_bitexact(wk, orc, lanes):
     n, k = 512, 40
-    eng = wk.Engine(n, seed=SEED, RandomizeStart=1, RandomizeMaterial=1)
+    eng = wk.Engine(n, seed=SEED, RandomizeStart=1, RandomizeMaterial=1, LanesPerWalker=lanes)
     envs, _, _ = oracle_envs(orc, eng, n)
     rng = np.random.default_rng(5)
     acts = rng.uniform(-1, 1, (k, n, 4)).astype(F)
@@ -100,9 +106,10 @@ def test_many_envs_multi_step_bitexact(wk, orc):
     np.testing.assert_array_equal(eng.get_state(), np.stack([e.dump() for e in envs]))
 
 
-def test_reset_mask_and_materials(wk, orc):
+@lanes_param
+def test_reset_mask_and_materials(wk, orc, lanes):
     n = 16
-    eng = wk.Engine(n, seed=SEED)
+    eng = wk.Engine(n, seed=SEED, LanesPerWalker=lanes)
     mats = np.array([0, 1, 2] * 5 + [0], np.int32)
     eng.set_materials(mats)
     acts = np.random.default_rng(2).uniform(-1, 1, (20, n, 4)).astype(F)
@@ -139,10 +146,13 @@ def test_policy_sample_matches_oracle(wk, orc, eng64):
     np.testing.assert_allclose(v, [ag.value(o) for o in obs], rtol=1e-5, atol=1e-6)
 
 
-def test_rollout_physics_replays_exactly(wk, orc, eng64):
+@lanes_param
+def test_rollout_physics_replays_exactly(wk, orc, lanes):
     """Policy rollout on the GPU; the oracle replays the recorded (unclipped) actions and
     must reproduce states, rewards and dones bit-exactly; the recorded actions match the
     oracle's own sampling within fp32 tolerance."""
+    eng64 = wk.Engine(64, seed=SEED, RandomizeStart=1, RandomizeMaterial=1, Horizon=32,
+                      LanesPerWalker=lanes)
     ag = orc.Agent(seed=SEED)
     eng64.set_weights(ag.params())
     eng64.reset()
@@ -169,10 +179,11 @@ def test_rollout_physics_replays_exactly(wk, orc, eng64):
         np.testing.assert_array_equal(tr["advantages"][:, i], adv)
 
 
-def test_rollout_sampling_matches_oracle(wk, orc):
+@lanes_param
+def test_rollout_sampling_matches_oracle(wk, orc, lanes):
     ag = orc.Agent(seed=SEED)
     n, T = 32, 4
-    eng = wk.Engine(n, seed=SEED, Horizon=T)
+    eng = wk.Engine(n, seed=SEED, Horizon=T, LanesPerWalker=lanes)
     eng.set_weights(ag.params())
     eng.rollout(T)
     tr = eng.get_trajectory(T)
@@ -282,3 +293,25 @@ def test_step_device_pointers(wk):
     np.testing.assert_array_equal(obs.cpu().numpy(), o2)
     np.testing.assert_array_equal(rew.cpu().numpy(), r2)
     np.testing.assert_array_equal(done.cpu().numpy(), d2)
+
+
+def test_mappings_agree_at_scale(wk):
+    """Size-independent property at the bench's per-GPU size: the three physics mappings
+    (and the fused policy) produce bit-identical rollouts, trajectories and states."""
+    n, T = 65536, 4
+    outs = []
+    for lanes in LANES:
+        eng = wk.Engine(n, seed=SEED, Horizon=T, RandomizeStart=1, RandomizeMaterial=1,
+                        LanesPerWalker=lanes)
+        eng.rollout(T)
+        tr = eng.get_trajectory(T)
+        outs.append((eng.get_state(), tr["states"], tr["rewards"], tr["dones"], tr["actions"]))
+        eng.close()
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            np.testing.assert_array_equal(a, b)
+
+
+def test_invalid_lanes_rejected(wk):
+    with pytest.raises(wk.WkError):
+        wk.Engine(4, seed=SEED, LanesPerWalker=3)
