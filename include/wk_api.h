@@ -219,6 +219,13 @@ int wk_train_batch(wk_ctx* ctx, int B, float b_div, const float* states, const f
                    const float* logp_old, const float* returns, const float* adv,
                    float* critic_diag, float* actor_diag, float* grads_out, int apply_adam,
                    int* skipped);
+/* The same minibatch gradient as computed inside wk_ppo_update (matrix-core kernel,
+ * samples summed in 16-sample MFMA blocks -- a different fp32 association than
+ * Train(Batch)'s sequential loop, PPOAgent.cs:228-335); no Adam step. */
+int wk_minibatch_gradient(wk_ctx* ctx, int B, float b_div, const float* states,
+                          const float* actions, const float* logp_old, const float* returns,
+                          const float* adv, float* critic_diag, float* actor_diag,
+                          float* grads_out, int* skipped);
 
 /* multi-GPU: RCCL communicator over the ranks' contexts (one per GPU) */
 int wk_comm_unique_id(uint8_t* id /* 128 bytes */);

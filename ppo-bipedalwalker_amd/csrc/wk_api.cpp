@@ -628,9 +628,11 @@ int wk_set_trajectory(wk_ctx* c, int horizon, const float* s, const float* a, co
 }
 
 // one minibatch: gradient kernel -> ordered block reduction -> [RCCL all-reduce] -> Adam
+// wpb == 0: the matrix-core kernel (wk_ppo_mfma.hip); wpb >= 1: the lane-per-neuron
+// kernel (wk_ppo.hip; wpb == 1 visits the samples in minibatch order)
 static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
-  const int per_block = wpb * g.spw;
-  const int nblocks = (g.samples + per_block - 1) / per_block;
+  const int nblocks = wpb == 0 ? wk::ppo_grad_mfma_blocks(g.samples)
+                               : (g.samples + wpb * g.spw - 1) / (wpb * g.spw);
   // block slabs followed by the stage-1 group sums of the ordered reduction
   const size_t need = ((size_t)nblocks + wk::grad_reduce_groups(nblocks)) * wk::SLAB;
   if (c->partial_floats < need) {
@@ -643,7 +645,8 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   g.partial = c->partial;
   {
     ProfScope ps(c, PK_GRAD);
-    HIPCHK(c, wk::launch_ppo_grad(g, wpb, nblocks, c->stream));
+    HIPCHK(c, wpb == 0 ? wk::launch_ppo_grad_mfma(g, nblocks, c->stream)
+                       : wk::launch_ppo_grad(g, wpb, nblocks, c->stream));
   }
   {
     ProfScope ps(c, PK_REDUCE);
@@ -700,9 +703,8 @@ int wk_ppo_update(wk_ctx* c, const wk_ppo_args* args, float* critic_diag, float*
   const uint32_t pool = (uint32_t)((size_t)c->n * c->T_valid);
   const int nmb = (int)(pool / (uint32_t)M);  // remainder dropped (PPOAgent.cs:506)
   if (nmb <= 0) { SETERR(c, "minibatch %d larger than the pool %u", M, pool); return WK_ERR_ARG; }
-  const int wpb = 4;
-  int spw = (M + wpb * 256 - 1) / (wpb * 256);
-  if (spw < 1) spw = 1;
+  const int wpb = 0;  // matrix cores
+  const int spw = 0;
   wk::GradArgs g = grad_base(c);
   g.states = c->ts; g.actions = c->ta; g.logp_old = c->tlp; g.returns = c->tret; g.adv = c->tadv;
   g.pool = pool;
@@ -726,9 +728,9 @@ int wk_ppo_update(wk_ctx* c, const wk_ppo_args* args, float* critic_diag, float*
   return WK_OK;
 }
 
-int wk_train_batch(wk_ctx* c, int B, float b_div, const float* s, const float* a, const float* lpo,
-                   const float* ret, const float* adv, float* cd, float* ad, float* grads_out,
-                   int apply_adam, int* skipped) {
+static int batch_impl(wk_ctx* c, int wpb, int B, float b_div, const float* s, const float* a,
+                      const float* lpo, const float* ret, const float* adv, float* cd, float* ad,
+                      float* grads_out, int apply_adam, int* skipped) {
   if (!c || B <= 0 || !s || !a || !lpo || !ret || !adv) return WK_ERR_ARG;
   const size_t bs = sizeof(float) * B;
   const size_t total = bs * (12 + 4 + 4 + 1 + 1) + 256;
@@ -750,9 +752,9 @@ int wk_train_batch(wk_ctx* c, int B, float b_div, const float* s, const float* a
   g.base = 0;
   g.use_perm = 0;
   g.samples = B;
-  g.spw = B;  // one wave, samples in order: the reference's sequential accumulation
+  g.spw = B;  // wpb 1: one wave, samples in order (the reference's sequential sums)
   g.b_div = b_div;
-  int r = minibatch(c, g, 1, apply_adam);
+  int r = minibatch(c, g, wpb, apply_adam);
   if (r) return r;
   std::vector<float> slab(wk::SLAB);
   HIPCHK(c, hipMemcpyAsync(slab.data(), c->grad, sizeof(float) * slab.size(), hipMemcpyDeviceToHost, c->stream));
@@ -762,6 +764,18 @@ int wk_train_batch(wk_ctx* c, int B, float b_div, const float* s, const float* a
   if (ad) *ad = slab[wk::NPARAM + 1];
   if (skipped) *skipped = (int)slab[wk::NPARAM + 2];
   return WK_OK;
+}
+
+int wk_train_batch(wk_ctx* c, int B, float b_div, const float* s, const float* a, const float* lpo,
+                   const float* ret, const float* adv, float* cd, float* ad, float* grads_out,
+                   int apply_adam, int* skipped) {
+  return batch_impl(c, 1, B, b_div, s, a, lpo, ret, adv, cd, ad, grads_out, apply_adam, skipped);
+}
+
+int wk_minibatch_gradient(wk_ctx* c, int B, float b_div, const float* s, const float* a,
+                          const float* lpo, const float* ret, const float* adv, float* cd,
+                          float* ad, float* grads_out, int* skipped) {
+  return batch_impl(c, 0, B, b_div, s, a, lpo, ret, adv, cd, ad, grads_out, 0, skipped);
 }
 
 int wk_comm_unique_id(uint8_t* id) {

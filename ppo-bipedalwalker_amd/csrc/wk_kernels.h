@@ -24,7 +24,7 @@ struct PairTraceDev {
 };
 
 struct StepArgs {
-  float* st;                 // SoA state [NSTATE][n]
+  float* st;                 // walker state records [n][NSTATE]
   const float* dxoff;        // [n] start offset (x = 125 + dx)
   const int32_t* mat;        // [n] material id
   uint32_t* rng_t;           // [n] per-env env-step counter (Philox counter)
@@ -79,6 +79,8 @@ hipError_t launch_policy(const EnvParams& P, const float* W, float lp_const, int
 hipError_t launch_returns(int n, int T, int use_gae, float gamma, float lambda, const float* r,
                           const float* v, const uint8_t* d, float* ret, float* adv, hipStream_t s);
 hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t s);
+hipError_t launch_ppo_grad_mfma(const GradArgs& g, int nblocks, hipStream_t s);
+int ppo_grad_mfma_blocks(int samples);
 hipError_t launch_grad_reduce(const float* partial, int nblocks, float* part2, float* grad,
                               hipStream_t s);
 int grad_reduce_groups(int nblocks);

@@ -1,0 +1,412 @@
+// wk_ppo_mfma.hip -- the PPO minibatch gradient on the CDNA4 matrix cores (gfx950).
+//
+// Same math as k_ppo_grad (PPOAgent.Train(Batch), Walker/PPO/PPOAgent.cs:218-346 with
+// NeuralNetwork.FeedForward / FeedBack, NeuralNetwork.cs:52-82, DenseLayer.cs:82-120,
+// ActivationLayer.cs:18-21), restated as batched GEMMs over chunks of 16 samples with
+// v_mfma_f32_16x16x4_f32 (exact fp32 products and sums; only the association of each
+// sum over k / over samples differs from the sequential reference, which the parity
+// tests bound).  Per wave and chunk:
+//
+//   forward   Z1^T = W1 S^T, Zc1^T = Wc1 S^T      (M 64, K 12, N 16)
+//             Z2^T = W2 H1^T                      (M 64, K 64, N 16; B = Z1's D registers)
+//             z3, V: 64-long dots on the VALU, summed over the 4 lane groups
+//   loss      per (sample, action dim) in lane (n, g = d): ratio, clip, dmu, dV
+//   backward  gh2 = W3^T gz3 (VALU), dW3|dWc2 += [gz3; dV]^T [H2 | Hc1]  (M 16, K 16, N 128)
+//             dW2 += gz2^T H1                     (M 64, K 16 samples, N 64)
+//             gh1^T = W2^T gz2^T                  (chained, B = gz2's registers)
+//             dW1|db1 += gz1^T [S | 1], dWc1|dbc1 likewise (M 64, K 16, N 16)
+//
+// Operand layouts of v_mfma_f32_16x16x4_f32 (probed, scripts/probe/mfma_layout.hip):
+// lane l = 16 g + n holds A[n][g], B[g][n] and D[4 g + r][n] (r = 0..3).  With samples
+// on n and neurons 16 Mt + 4 g + r on (g, r), a layer's D registers are directly the
+// B operand of the next layer when its K steps are ordered (Mt, r) -- the weights are
+// pre-swizzled into LDS in that order.  Weight-gradient GEMMs need samples on K, so
+// activations / gradients pass through small per-wave [16][80] LDS tiles (row stride
+// 80 = 16 mod 64 banks: conflict-free operand reads).  Accumulators stay in registers
+// across chunks; waves fold into the block slab in wave order and blocks write partial
+// slabs for the ordered reduction (bit-reproducible, no atomics).
+#include "wk_common.h"
+#include "wk_kernels.h"
+
+namespace wk {
+
+#define DEV __device__ __forceinline__
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+namespace mf {
+enum : int {
+  AW1F = 0,              // [Mt 4][t 3][lane 64]        W1[16Mt + n][4t + g]
+  CW1F = AW1F + 768,     // critic W1, same order
+  W2F = CW1F + 768,      // [Mt 4][Mp 4][lane 64][r 4]  W2[16Mt + n][16Mp + 4g + r]
+  W2B = W2F + 4096,      // [Mk 4][Mj 4][lane 64][r 4]  W2[16Mj + 4g + r][16Mk + n]
+  W3 = W2B + 4096,       // [4][64]
+  WC2 = W3 + 256,        // [64]
+  BA1 = WC2 + 64, BA2 = BA1 + 64, BC1 = BA2 + 64, BA3 = BC1 + 64, BC2 = BA3 + 4,
+  WEND = BC2 + 4,
+  RS = 80,               // row stride of a [16 samples][64] tile
+  C_H1 = 0, C_HC1 = C_H1 + 16 * RS, C_H2 = C_HC1 + 16 * RS, C_G2 = C_H2 + 16 * RS,
+  C_SX = C_G2 + 16 * RS,  // [16][16]: 12 features, 1.0 (bias column), 0, 0, 0
+  C_G3 = C_SX + 256,      // [16][16]: gz3 (4 dims), dV, zeros
+  CHUNK = C_G3 + 256,
+  C_G1 = C_H2, C_GC1 = C_HC1,  // backward tiles reuse the forward ones
+  WAVES = 4
+};
+static_assert(WEND % 4 == 0, "16-byte aligned chunk tiles");
+static_assert(WAVES * CHUNK >= SLAB, "slab fits the chunk tiles");
+}  // namespace mf
+
+DEV float mf_lrelu(float z) {  // ActivationLayer LeakyReLU(0.2): Math.Max(0.2 z, z)
+  const float a = 0.2f * z;
+  if (a != z) { if (!__builtin_isnan(a)) return z < a ? a : z; return a; }
+  return __builtin_signbit(z) ? a : z;
+}
+DEV float mf_dlrelu(float z) { return z < 0.0f ? 0.2f : 1.0f; }
+DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+DEV f4 mfma(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+// sum over the 16 lanes of a DPP row (all lanes get the total)
+DEV float row_sum16(float v) {
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+__global__ __launch_bounds__(64 * mf::WAVES) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_ppo_grad_mfma(GradArgs ga) {
+  using namespace mf;
+  extern __shared__ float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = lane & 15, g = lane >> 4;
+
+  // ---- stage the pre-swizzled weights ----
+  const float* W = ga.W;
+  for (int e = tid; e < 768; e += 64 * WAVES) {
+    const int Mt = e / 192, t = (e / 64) % 3, l = e & 63;
+    const int m = 16 * Mt + (l & 15), k = 4 * t + (l >> 4);
+    lds[AW1F + e] = W[OFF_A_W1 + m * 12 + k];
+    lds[CW1F + e] = W[OFF_C_W1 + m * 12 + k];
+  }
+  for (int e = tid; e < 4096; e += 64 * WAVES) {
+    const int A = e >> 10, B = (e >> 8) & 3, l = (e >> 2) & 63, r = e & 3;
+    lds[W2F + e] = W[OFF_A_W2 + (16 * A + (l & 15)) * 64 + 16 * B + 4 * (l >> 4) + r];
+    lds[W2B + e] = W[OFF_A_W2 + (16 * B + 4 * (l >> 4) + r) * 64 + 16 * A + (l & 15)];
+  }
+  for (int e = tid; e < 256; e += 64 * WAVES) lds[W3 + e] = W[OFF_A_W3 + e];
+  for (int e = tid; e < 64; e += 64 * WAVES) {
+    lds[WC2 + e] = W[OFF_C_W2 + e];
+    lds[BA1 + e] = W[OFF_A_B1 + e];
+    lds[BA2 + e] = W[OFF_A_B2 + e];
+    lds[BC1 + e] = W[OFF_C_B1 + e];
+  }
+  if (tid < 4) lds[BA3 + tid] = W[OFF_A_B3 + tid];
+  if (tid == 0) lds[BC2] = W[OFF_C_B2];
+  float* cb = lds + WEND + wave * CHUNK;
+  for (int e = lane; e < 256; e += 64) cb[C_G3 + e] = 0.0f;
+  __syncthreads();
+
+  // ---- accumulators (registers, across chunks) ----
+  const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+  f4 a2[4][4], a1[4], a1c[4], a3[8];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    a1[i] = z4; a1c[i] = z4;
+#pragma unroll
+    for (int j = 0; j < 4; j++) a2[i][j] = z4;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) a3[i] = z4;
+  float db2[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) db2[i] = 0.0f;
+  float db3 = 0.0f, dbc2 = 0.0f, diagC = 0.0f, diagA = 0.0f, skipped = 0.0f;
+
+  const float b3g = lds[BA3 + g], bc2 = lds[BC2];
+  const int nchunks = (ga.samples + 15) / 16;
+  const int nw = gridDim.x * WAVES;
+#pragma unroll 1
+  for (int c = blockIdx.x * WAVES + wave; c < nchunks; c += nw) {
+    // ---- gather (CreateBatches, PPOAgent.cs:512-533) ----
+    const int pos = c * 16 + n;
+    const bool valid = pos < ga.samples;
+    uint32_t idx = ga.base + (uint32_t)(valid ? pos : 0);
+    if (ga.use_perm) idx = perm_apply(idx, ga.pk);
+    f4 sv = {1.0f, 0.0f, 0.0f, 0.0f};  // lane group 3: the bias column
+    if (g < 3) sv = *(const f4*)(ga.states + (size_t)idx * 12 + 4 * g);
+    *(f4*)(cb + C_SX + n * 16 + 4 * g) = sv;
+    const float act = ga.actions[(size_t)idx * 4 + g];
+    const float lpo = ga.logp_old[(size_t)idx * 4 + g];
+    const float ret = ga.returns[idx];
+    const float adv = ga.adv[idx];
+    wave_sync();
+
+    // ---- layer 1, actor and critic ----
+    float sB[3];
+#pragma unroll
+    for (int t = 0; t < 3; t++) sB[t] = cb[C_SX + n * 16 + 4 * t + g];
+    f4 z1[4], zc1[4], h1[4];
+#pragma unroll
+    for (int Mt = 0; Mt < 4; Mt++) {
+      f4 acc = z4, accc = z4;
+#pragma unroll
+      for (int t = 0; t < 3; t++) {
+        acc = mfma(lds[AW1F + (Mt * 3 + t) * 64 + lane], sB[t], acc);
+        accc = mfma(lds[CW1F + (Mt * 3 + t) * 64 + lane], sB[t], accc);
+      }
+      f4 hc;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int j = 16 * Mt + 4 * g + r;
+        acc[r] = acc[r] + lds[BA1 + j];
+        accc[r] = accc[r] + lds[BC1 + j];
+        h1[Mt][r] = mf_lrelu(acc[r]);
+        hc[r] = mf_lrelu(accc[r]);
+      }
+      z1[Mt] = acc;
+      zc1[Mt] = accc;
+      *(f4*)(cb + C_H1 + n * RS + 16 * Mt + 4 * g) = h1[Mt];
+      *(f4*)(cb + C_HC1 + n * RS + 16 * Mt + 4 * g) = hc;
+    }
+    // ---- layer 2 (B operand = layer 1's D registers) ----
+    f4 z2[4], h2[4];
+#pragma unroll
+    for (int Mt = 0; Mt < 4; Mt++) {
+      f4 acc = z4;
+#pragma unroll
+      for (int Mp = 0; Mp < 4; Mp++) {
+        const f4 w = *(const f4*)(lds + W2F + ((Mt * 4 + Mp) * 64 + lane) * 4);
+#pragma unroll
+        for (int r = 0; r < 4; r++) acc = mfma(w[r], h1[Mp][r], acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        acc[r] = acc[r] + lds[BA2 + 16 * Mt + 4 * g + r];
+        h2[Mt][r] = mf_lrelu(acc[r]);
+      }
+      z2[Mt] = acc;
+      *(f4*)(cb + C_H2 + n * RS + 16 * Mt + 4 * g) = h2[Mt];
+    }
+    // ---- output rows: actor z3[0..3] on h2, critic V on hc1 ----
+    float p3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, pv = 0.0f;
+#pragma unroll
+    for (int Mt = 0; Mt < 4; Mt++) {
+      const f4 hc = *(const f4*)(cb + C_HC1 + n * RS + 16 * Mt + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int k = 16 * Mt + 4 * g + r;
+#pragma unroll
+        for (int d = 0; d < 4; d++) p3[d] = p3[d] + lds[W3 + d * 64 + k] * h2[Mt][r];
+        pv = pv + lds[WC2 + k] * hc[r];
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      p3[d] = p3[d] + __shfl_xor(p3[d], 16);
+      p3[d] = p3[d] + __shfl_xor(p3[d], 32);
+    }
+    pv = pv + __shfl_xor(pv, 16);
+    pv = pv + __shfl_xor(pv, 32);
+    const float z3 = (g == 0 ? p3[0] : g == 1 ? p3[1] : g == 2 ? p3[2] : p3[3]) + b3g;
+    const float V = pv + bc2;
+
+    // ---- PPO derivative for action dimension d = g (PPOAgent.cs:234-326) ----
+    const float mean = tanhf(z3);
+    float criticLoss = 2.0f * (V - ret);
+    float fr = (act - mean) / ga.std_;
+    fr *= fr;
+    fr /= 2.0f;
+    const float lp = ga.lp_const - fr;
+    const float rr = expf(lp - lpo);
+    const float cr = rr >= ga.upper ? ga.upper : (rr <= ga.lower ? ga.lower : rr);
+    const float cra = cr * adv, ra = rr * adv;
+    const float partA = (ra <= cra ? 1.0f : 0.0f) * adv;
+    const float partB = (cra < ra ? 1.0f : 0.0f) * adv;
+    const float partC = (rr >= ga.lower && rr <= ga.upper) ? 1.0f : 0.0f;
+    float l = partA + (partB * partC);
+    l = l * -1.0f;
+    const float eo = expf(lpo);
+    float zd = eo == 0.0f ? 1.0f : 0.0f;  // Matrix.HadamardDivision throws -> sample skipped
+    zd = fmaxf(zd, __shfl_xor(zd, 16));
+    zd = fmaxf(zd, __shfl_xor(zd, 32));
+    const bool use = valid && zd == 0.0f;
+    const float lcd = l / eo;
+    const float prob = expf(lp);
+    const float frac = (act - mean) / (ga.std_ * ga.std_);
+    float actorLoss = (prob * frac) * lcd;
+    criticLoss = use ? criticLoss / ga.b_div : 0.0f;
+    actorLoss = use ? actorLoss / ga.b_div : 0.0f;
+    const float th = tanhf(z3);
+    const float gz3 = actorLoss * (1.0f - (th * th));
+    float al[4], q[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      al[d] = __shfl(actorLoss, n + 16 * d);
+      q[d] = __shfl(gz3, n + 16 * d);
+    }
+    if (g == 0) {
+      diagC += criticLoss;
+      diagA += use ? ((((0.0f + al[0]) + al[1]) + al[2]) + al[3]) / 4.0f : 0.0f;
+      skipped += (valid && !use) ? 1.0f : 0.0f;
+      dbc2 += criticLoss;
+      cb[C_G3 + n * 16 + 4] = criticLoss;
+    }
+    db3 += gz3;
+    cb[C_G3 + n * 16 + g] = gz3;
+    // ---- gh2 = W3^T gz3 -> gz2 ----
+    f4 gz2[4];
+#pragma unroll
+    for (int Mt = 0; Mt < 4; Mt++) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int k = 16 * Mt + 4 * g + r;
+        float gh = 0.0f;
+#pragma unroll
+        for (int d = 0; d < 4; d++) gh = gh + lds[W3 + d * 64 + k] * q[d];
+        gz2[Mt][r] = gh * mf_dlrelu(z2[Mt][r]);
+        db2[Mt * 4 + r] += gz2[Mt][r];
+      }
+      *(f4*)(cb + C_G2 + n * RS + 16 * Mt + 4 * g) = gz2[Mt];
+    }
+    wave_sync();
+    // ---- dW3 | dWc2 += [gz3; dV]^T [H2 | Hc1]; dW2 += gz2^T H1 (samples on K) ----
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int s = 4 * t + g;
+      const float av = cb[C_G3 + s * 16 + n];
+#pragma unroll
+      for (int Nt = 0; Nt < 4; Nt++) {
+        a3[Nt] = mfma(av, cb[C_H2 + s * RS + 16 * Nt + n], a3[Nt]);
+        a3[Nt + 4] = mfma(av, cb[C_HC1 + s * RS + 16 * Nt + n], a3[Nt + 4]);
+      }
+      float ag[4], bh[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        ag[i] = cb[C_G2 + s * RS + 16 * i + n];
+        bh[i] = cb[C_H1 + s * RS + 16 * i + n];
+      }
+#pragma unroll
+      for (int Mj = 0; Mj < 4; Mj++)
+#pragma unroll
+        for (int Nk = 0; Nk < 4; Nk++) a2[Mj][Nk] = mfma(ag[Mj], bh[Nk], a2[Mj][Nk]);
+    }
+    wave_sync();  // H2 / Hc1 reads done before G1 / Gc1 overwrite them
+    // ---- gh1^T = W2^T gz2^T (B = gz2 registers) -> gz1; critic gzc1 ----
+#pragma unroll
+    for (int Mk = 0; Mk < 4; Mk++) {
+      f4 acc = z4;
+#pragma unroll
+      for (int Mj = 0; Mj < 4; Mj++) {
+        const f4 w = *(const f4*)(lds + W2B + ((Mk * 4 + Mj) * 64 + lane) * 4);
+#pragma unroll
+        for (int r = 0; r < 4; r++) acc = mfma(w[r], gz2[Mj][r], acc);
+      }
+      f4 gz1, gzc1;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int k = 16 * Mk + 4 * g + r;
+        gz1[r] = acc[r] * mf_dlrelu(z1[Mk][r]);
+        const float ghc1 = 0.0f + lds[WC2 + k] * criticLoss;  // same in the sample's 4 lanes
+        gzc1[r] = ghc1 * mf_dlrelu(zc1[Mk][r]);
+      }
+      *(f4*)(cb + C_G1 + n * RS + 16 * Mk + 4 * g) = gz1;
+      *(f4*)(cb + C_GC1 + n * RS + 16 * Mk + 4 * g) = gzc1;
+    }
+    wave_sync();
+    // ---- dW1 | db1, dWc1 | dbc1 += gz1^T [S | 1] ----
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int s = 4 * t + g;
+      const float bx = cb[C_SX + s * 16 + n];
+#pragma unroll
+      for (int Mj = 0; Mj < 4; Mj++) {
+        a1[Mj] = mfma(cb[C_G1 + s * RS + 16 * Mj + n], bx, a1[Mj]);
+        a1c[Mj] = mfma(cb[C_GC1 + s * RS + 16 * Mj + n], bx, a1c[Mj]);
+      }
+    }
+    wave_sync();  // the next chunk rewrites every tile
+  }
+
+  // ---- per-lane sums over the 16 sample lanes of each row ----
+#pragma unroll
+  for (int i = 0; i < 16; i++) db2[i] = row_sum16(db2[i]);
+  db3 = row_sum16(db3);
+  dbc2 = row_sum16(dbc2);
+  diagC = row_sum16(diagC);
+  diagA = row_sum16(diagA);
+  skipped = row_sum16(skipped);
+
+  // ---- fold the waves into the block slab in wave order ----
+  __syncthreads();
+  float* slab = lds + WEND;
+  for (int i = tid; i < SLAB; i += 64 * WAVES) slab[i] = 0.0f;
+  __syncthreads();
+#pragma unroll 1
+  for (int w = 0; w < WAVES; w++) {
+    if (w == wave) {
+#pragma unroll
+      for (int Mj = 0; Mj < 4; Mj++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int j = 16 * Mj + 4 * g + r;
+#pragma unroll
+          for (int Nk = 0; Nk < 4; Nk++) slab[OFF_A_W2 + j * 64 + 16 * Nk + n] += a2[Mj][Nk][r];
+          if (n < 12) {
+            slab[OFF_A_W1 + j * 12 + n] += a1[Mj][r];
+            slab[OFF_C_W1 + j * 12 + n] += a1c[Mj][r];
+          } else if (n == 12) {
+            slab[OFF_A_B1 + j] += a1[Mj][r];
+            slab[OFF_C_B1 + j] += a1c[Mj][r];
+          }
+        }
+#pragma unroll
+      for (int Nt = 0; Nt < 4; Nt++) {
+        if (g == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; r++) slab[OFF_A_W3 + r * 64 + 16 * Nt + n] += a3[Nt][r];
+        } else if (g == 1) {
+          slab[OFF_C_W2 + 16 * Nt + n] += a3[Nt + 4][0];
+        }
+      }
+      if (n == 0) {
+#pragma unroll
+        for (int Mt = 0; Mt < 4; Mt++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) slab[OFF_A_B2 + 16 * Mt + 4 * g + r] += db2[Mt * 4 + r];
+        slab[OFF_A_B3 + g] += db3;
+        if (g == 0) {
+          slab[OFF_C_B2] += dbc2;
+          slab[NPARAM] += diagC;
+          slab[NPARAM + 1] += diagA;
+          slab[NPARAM + 2] += skipped;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* out = ga.partial + (size_t)blockIdx.x * SLAB;
+  for (int i = tid; i < SLAB; i += 64 * WAVES) out[i] = slab[i];
+}
+
+int ppo_grad_mfma_blocks(int samples) {
+  const int chunks = (samples + 15) / 16;
+  int blocks = (chunks + mf::WAVES - 1) / mf::WAVES;
+  return blocks < 256 ? blocks : 256;  // one block per CU; waves loop over the chunks
+}
+
+hipError_t launch_ppo_grad_mfma(const GradArgs& g, int nblocks, hipStream_t s) {
+  const size_t lds = sizeof(float) * (mf::WEND + mf::WAVES * mf::CHUNK);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k_ppo_grad_mfma,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k_ppo_grad_mfma, dim3(nblocks), dim3(64 * mf::WAVES), lds, s, g);
+  return hipGetLastError();
+}
+
+}  // namespace wk

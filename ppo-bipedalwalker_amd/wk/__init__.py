@@ -30,6 +30,7 @@ EXPORTS = [
     "wk_get_body_view", "wk_get_weights", "wk_set_weights", "wk_get_adam", "wk_set_adam",
     "wk_policy_sample", "wk_value", "wk_rollout", "wk_rollout_stats_get", "wk_get_trajectory",
     "wk_set_trajectory", "wk_compute_returns", "wk_ppo_update", "wk_train_batch",
+    "wk_minibatch_gradient",
     "wk_comm_unique_id", "wk_comm_init", "wk_allreduce_test", "wk_profile_enable",
     "wk_profile_get", "wk_profile_reset",
 ]
@@ -151,6 +152,7 @@ def load_library(path=None):
         "wk_compute_returns": (I, [P]),
         "wk_ppo_update": (I, [P, C.POINTER(PpoArgs), fp, fp]),
         "wk_train_batch": (I, [P, I, F, P, P, P, P, P, fp, fp, P, I, C.POINTER(C.c_int)]),
+        "wk_minibatch_gradient": (I, [P, I, F, P, P, P, P, P, fp, fp, P, C.POINTER(C.c_int)]),
         "wk_comm_unique_id": (I, [P]),
         "wk_comm_init": (I, [P, I, I, P]),
         "wk_allreduce_test": (I, [P, P, I]),
@@ -382,6 +384,18 @@ class Engine:
             self.h, int(B), float(B if b_div is None else b_div), _ptr(s), _ptr(a), _ptr(l),
             _ptr(r), _ptr(v), C.byref(cd), C.byref(ad), _ptr(grads), int(bool(apply_adam)),
             C.byref(sk)), "wk_train_batch")
+        return grads, cd.value, ad.value, sk.value
+
+    def minibatch_gradient(self, states, actions, logp_old, returns, adv, b_div=None):
+        """The matrix-core minibatch gradient wk_ppo_update applies (no Adam)."""
+        s, a, l, r, v = (_f32(states), _f32(actions), _f32(logp_old), _f32(returns), _f32(adv))
+        B = r.shape[0]
+        grads = np.empty(NPARAM, np.float32)
+        cd, ad, sk = C.c_float(), C.c_float(), C.c_int()
+        self._chk(self.lib.wk_minibatch_gradient(
+            self.h, int(B), float(B if b_div is None else b_div), _ptr(s), _ptr(a), _ptr(l),
+            _ptr(r), _ptr(v), C.byref(cd), C.byref(ad), _ptr(grads), C.byref(sk)),
+            "wk_minibatch_gradient")
         return grads, cd.value, ad.value, sk.value
 
     # -- multi-GPU --

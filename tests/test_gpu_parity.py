@@ -315,3 +315,28 @@ def test_mappings_agree_at_scale(wk):
 def test_invalid_lanes_rejected(wk):
     with pytest.raises(wk.WkError):
         wk.Engine(4, seed=SEED, LanesPerWalker=3)
+
+
+@pytest.mark.parametrize("B", [1, 37, 2048])
+def test_minibatch_gradient_mfma_vs_oracle(wk, orc, B):
+    """The matrix-core gradient (wk_ppo_update's kernel) against the oracle's sequential
+    Train(Batch) on the same samples: fp32 re-association only (16-sample MFMA blocks,
+    4-way split dots), so rtol 2e-4 / atol 2e-6 relative to the largest gradient."""
+    rng = np.random.default_rng(B)
+    ag = orc.Agent(seed=SEED)
+    eng = wk.Engine(4, seed=SEED)
+    eng.set_weights(ag.params())
+    S = rng.normal(0, 1, (B, 12)).astype(F)
+    A = rng.normal(0, 1, (B, 4)).astype(F)
+    L = rng.normal(-3, 1, (B, 4)).astype(F)
+    G = rng.normal(0, 5, B).astype(F)
+    Ad = rng.normal(0, 1, B).astype(F)
+    if B > 5:
+        L[5, 2] = -200.0  # exp(logp_old) == 0: HadamardDivision throws, sample skipped
+    g, cd, ad, sk = eng.minibatch_gradient(S, A, L, G, Ad)
+    og, ocd, oad, osk = ag.train_batch(S, A, L, G, Ad, b_div=B, apply_adam=False)
+    scale = np.abs(og).max()
+    np.testing.assert_allclose(g, og, rtol=2e-4, atol=2e-6 * scale)
+    assert sk == osk
+    assert cd == pytest.approx(ocd, rel=1e-4, abs=1e-6)
+    assert ad == pytest.approx(oad, rel=1e-4, abs=1e-6)
