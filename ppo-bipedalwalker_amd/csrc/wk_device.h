@@ -21,9 +21,44 @@ DEV V2 vmul(V2 a, float s) { return mk(a.x * s, a.y * s); }
 DEV V2 vdiv(V2 a, float d) { float f = 1.0f / d; return mk(a.x * f, a.y * f); }
 DEV V2 vneg(V2 a) { return mk(-a.x, -a.y); }
 DEV float vdot(V2 a, V2 b) { return a.x * b.x + a.y * b.y; }
-DEV float vlen(V2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
+// Correctly rounded sqrt / reciprocal without the library's rescaling and special-value
+// fixups.  For x >= 2^-96 HIP's sqrtf is v_sqrt_f32 plus a one-ulp round-to-nearest
+// correction (below), and for a divisor in [2^-48, 2^64] its v_div_scale / v_div_fmas /
+// v_div_fixup sequence reduces to the Newton-Raphson FMAs of rcp_core: the same ops, so the
+// same bits (checked exhaustively over every float in range, tests/cpp/fastmath_check.hip).
+// Smaller inputs (never produced by walker-scale geometry) take the library path.
+DEV float sqrt_core(float x) {
+  float s = __builtin_amdgcn_sqrtf(x);
+  const float sd = __uint_as_float(__float_as_uint(s) - 1u);
+  const float su = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
+  s = (rd <= 0.0f) ? sd : s;
+  s = (ru > 0.0f) ? su : s;
+  return s;
+}
+DEV float rcp_core(float d) {
+  float r = __builtin_amdgcn_rcpf(d);
+  const float e = __builtin_fmaf(-d, r, 1.0f);
+  r = __builtin_fmaf(e, r, r);
+  float q = r;  // 1 * r
+  float rem = __builtin_fmaf(-d, q, 1.0f);
+  q = __builtin_fmaf(rem, r, q);
+  rem = __builtin_fmaf(-d, q, 1.0f);
+  return __builtin_fmaf(rem, r, q);
+}
+DEV bool fast_domain(float x) { return x >= 0x1p-96f && x <= 0x1p126f; }
+DEV float sqrt_rn(float x) {
+  if (__builtin_expect(!fast_domain(x), 0)) return sqrtf(x);
+  return sqrt_core(x);
+}
+// 1.0f / sqrtf(x) with both roundings
+DEV float rsqrt_rn(float x) {
+  if (__builtin_expect(!fast_domain(x), 0)) return 1.0f / sqrtf(x);
+  return rcp_core(sqrt_core(x));
+}
+DEV float vlen(V2 a) { return sqrt_rn(a.x * a.x + a.y * a.y); }
 DEV V2 vnormalize(V2 a) {
-  float val = 1.0f / sqrtf(a.x * a.x + a.y * a.y);
+  float val = rsqrt_rn(a.x * a.x + a.y * a.y);
   return mk(a.x * val, a.y * val);
 }
 
@@ -157,36 +192,42 @@ DEV void project2(float ax, float ay, const Poly<NA>& A, const Poly<NB>& B, floa
   }
 }
 
-// AxisChecks(vectorA = P's edges, vectorB = Q): projections of P then Q on each axis
+// AxisChecks(vectorA = P's edges, vectorB = Q): projections of P then Q on each axis.
+// Branch-free: every axis is evaluated -- the loop's early `return false` only cuts
+// short a result whose normal / depth the caller discards -- a zero-length edge is
+// skipped by predication, and the first strict minimum wins exactly as in the loop.
+// (On an overlapping axis both differences are > 0, so Math.Min == v_min there.)
 template <int NP, int NQ>
-DEV bool axis_checks(const Poly<NP>& P, const Poly<NQ>& Q, V2& normal, float& depth) {
+DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, float& depth) {
 #pragma unroll
   for (int i = 0; i < NP; i++) {
     const int i1 = (i + 1) % NP;
-    float ex = P.x[i1] - P.x[i], ey = P.y[i1] - P.y[i];
+    const float ex = P.x[i1] - P.x[i], ey = P.y[i1] - P.y[i];
     V2 axis = mk(-ey, ex);
-    if (axis.x == 0.0f && axis.y == 0.0f) continue;
-    axis = vnormalize(axis);
+    const bool valid = !(axis.x == 0.0f && axis.y == 0.0f);
+    axis = vnormalize(axis);  // NaN for a zero edge: masked by `valid`
     float pmin, pmax, qmin, qmax;
     project2(axis.x, axis.y, P, Q, pmin, pmax, qmin, qmax);
-    float temp = net_minf(qmax - pmin, pmax - qmin);
-    bool overlapping = (pmin < qmax) && (qmin < pmax);
-    if (!overlapping) return false;
-    if (temp >= depth) continue;
-    depth = temp;
-    normal = axis;
+    const float temp = __builtin_fminf(qmax - pmin, pmax - qmin);
+    const bool overlapping = (pmin < qmax) && (qmin < pmax);
+    sep = sep || (valid && !overlapping);
+    const bool take = valid && overlapping && temp < depth;
+    depth = take ? temp : depth;
+    normal.x = take ? axis.x : normal.x;
+    normal.y = take ? axis.y : normal.y;
   }
-  return true;
 }
 
 template <int NA, int NB>
 DEV bool sat(const Poly<NA>& A, const Poly<NB>& B, V2& normal, float& depth) {
   normal = mk(0.0f, 0.0f);
   depth = FLT_MAX;
-  bool result = axis_checks(A, B, normal, depth) && axis_checks(B, A, normal, depth);
+  bool sep = false;
+  axis_pass(A, B, sep, normal, depth);
+  axis_pass(B, A, sep, normal, depth);
   V2 dir = mk(B.cx - A.cx, B.cy - A.cy);
   if (vdot(dir, normal) > 0.0f) normal = vmul(normal, -1.0f);
-  return result;
+  return !sep;
 }
 
 // ---------------- SAT, axes split over an L-lane row (L in {4, 8, 16}) ----------------

@@ -30,6 +30,20 @@
 
 namespace wk {
 
+// Optional per-region wave-time profile (build with -DWK_REGION_PROF; scripts/region_prof.py):
+// s_memtime deltas accumulated per wave, summed over waves into g_region_prof.
+#ifdef WK_REGION_PROF
+__device__ unsigned long long g_region_prof[16];
+struct RegionProf { uint64_t acc[8]; uint64_t t; };
+DEV void rp_mark(RegionProf* p, int r) {
+  if (p) { const uint64_t t = __builtin_amdgcn_s_memtime(); p->acc[r] += t - p->t; p->t = t; }
+}
+#else
+struct RegionProf {};
+DEV void rp_mark(RegionProf*, int) {}
+#endif
+enum { RP_JOINT, RP_INTEG, RP_AABB, RP_SAT, RP_CONTACT, RP_IMPULSE, RP_POLICY, RP_OTHER };
+
 struct EnvState {
   Poly<6> lll, llu, rll, rlu;
   Poly<5> body;
@@ -176,8 +190,10 @@ DEV void get_obs(const EnvState& s, float o[12]) {
 // (Bodies/RigidBody.cs:66-96); B may be the static floor.
 template <int NA, int NB, bool BSTATIC, bool TRACE, int L>
 DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB,
-                      bool& colA, PairTraceDev* tr, int pi, int sub) {
-  if (!aabb_overlap(A, B)) return;
+                      bool& colA, PairTraceDev* tr, int pi, int sub, RegionProf* rp = nullptr) {
+  const bool ov = aabb_overlap(A, B);
+  rp_mark(rp, RP_AABB);
+  if (!ov) return;
   if (TRACE && tr) tr->aabb_hit[pi] = 1;
   if (BSTATIC) colA = true;  // body._isFloor -> Collided = true (:75)
   V2 n;
@@ -185,9 +201,11 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   bool hit;
   if constexpr (L > 1) hit = sat_row<L>(A, B, sub, n, depth);
   else hit = sat(A, B, n, depth);
+  rp_mark(rp, RP_SAT);
   if (!hit) return;
   V2 c0, c1;
   int nc = contact_points(A, B, n, c0, c1);
+  rp_mark(rp, RP_CONTACT);
   if (TRACE && tr) {
     tr->sat_hit[pi] = 1;
     tr->n_contacts[pi] = (uint8_t)nc;
@@ -218,6 +236,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   if (TRACE && tr) { tr->impulse[pi][0] = j; tr->impulse[pi][1] = jf; }
   apply_impulses<BSTATIC>(bA, bB, n, j, rA, rB);
   apply_impulses<BSTATIC>(bA, bB, tangent, jf, rAF, rBF);
+  rp_mark(rp, RP_IMPULSE);
 }
 
 // Joint.Step (Objects/RigidBodies/Joint.cs:31-41); ResolveJoint swaps the bodies (:40)
@@ -684,7 +703,8 @@ DEV void get_obs_side(const SideState& s, int side, float o[12]) {
 
 template <bool TRACE>
 DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
-                      PairTraceDev* tr, int side) {
+                      PairTraceDev* tr, int side, RegionProf* rp) {
+  rp_mark(rp, RP_OTHER);
   Poly<4> fl;
   floor_poly(fl);
   Dyn dfl;
@@ -696,24 +716,33 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
   if (side == 1) joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.up, s.dup, mp, tr, 1);
   bcast_torso<0xF5>(s.body, s.dbody);
   joint_step<6, 6, 2, 3, TRACE>(s.up, s.dup, mp, s.lo, s.dlo, mp, tr, 2 + side);
-  // this leg's RigidBody.Step calls (lower then upper), floor-first after a reset
+  rp_mark(rp, RP_JOINT);
+  // this leg's RigidBody.Step calls (lower then upper); a segment's two candidates run
+  // floor-first after a reset, floor-last in episode 0: three slots keep a wave with
+  // both kinds of walkers at three pair evaluations instead of four
   const int pb = side ? 5 : 0;
   integrate(s.lo, s.dlo, dt, adx, ady);
+  rp_mark(rp, RP_INTEG);
 #pragma unroll 1
-  for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1>(s.lo, s.dlo, mp, fl, dfl, mf, s.clo, tr, pb + 1, 0);
-    else resolve_pair<6, 6, false, TRACE, 1>(s.lo, s.dlo, mp, s.up, s.dup, mp, s.clo, tr, pb + 0, 0);
+  for (int q = 0; q < 3; q++) {  // [floor if post], other segment, [floor if episode 0]
+    if (q == 1) resolve_pair<6, 6, false, TRACE, 1>(s.lo, s.dlo, mp, s.up, s.dup, mp, s.clo, tr, pb + 0, 0, rp);
+    else if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1>(s.lo, s.dlo, mp, fl, dfl, mf, s.clo, tr, pb + 1, 0, rp);
+    rp_mark(rp, RP_OTHER);
   }
   integrate(s.up, s.dup, dt, adx, ady);
+  rp_mark(rp, RP_INTEG);
 #pragma unroll 1
-  for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1>(s.up, s.dup, mp, fl, dfl, mf, s.cup, tr, pb + 3, 0);
-    else resolve_pair<6, 6, false, TRACE, 1>(s.up, s.dup, mp, s.lo, s.dlo, mp, s.cup, tr, pb + 2, 0);
+  for (int q = 0; q < 3; q++) {
+    if (q == 1) resolve_pair<6, 6, false, TRACE, 1>(s.up, s.dup, mp, s.lo, s.dlo, mp, s.cup, tr, pb + 2, 0, rp);
+    else if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1>(s.up, s.dup, mp, fl, dfl, mf, s.cup, tr, pb + 3, 0, rp);
+    rp_mark(rp, RP_OTHER);
   }
   // the torso's step, replicated in both lanes (traced by the left lane)
   integrate(s.body, s.dbody, dt, adx, ady);
+  rp_mark(rp, RP_INTEG);
   resolve_pair<5, 4, true, TRACE, 1>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody,
-                                     side == 0 ? tr : nullptr, 4, 0);
+                                     side == 0 ? tr : nullptr, 4, 0, rp);
+  rp_mark(rp, RP_OTHER);
 }
 
 DEV bool side_finite(const SideState& s) {
@@ -742,10 +771,18 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArg
   const uint32_t gid = (uint32_t)(P.env_offset + e);
   uint32_t t = A.rng_t[e];
   uint32_t fault = 0;
+#ifdef WK_REGION_PROF
+  RegionProf rpv = {};
+  rpv.t = __builtin_amdgcn_s_memtime();
+  RegionProf* rp = &rpv;
+#else
+  RegionProf* rp = nullptr;
+#endif
 
 #pragma unroll 1
   for (int k = 0; k < A.k_steps; k++) {
     float a[4], lp[4], obs[12];
+    rp_mark(rp, RP_OTHER);
     if (POLICY) {
       get_obs_side(s, side, obs);
       float mean[4];
@@ -768,6 +805,7 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArg
 #pragma unroll
       for (int d = 0; d < 4; d++) a[d] = A.actions[((size_t)k * n + e) * 4 + d];
     }
+    rp_mark(rp, RP_POLICY);
     s.steps++;
     // Clip + Joint.SetTorque: joint `side` drives this upper leg, joint 2+side the lower
     {
@@ -778,7 +816,7 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArg
 #pragma unroll 1
     for (int it = 0; it < P.iterations; it++) {
       PairTraceDev* tr = TRACE ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
-      substep_side<TRACE>(s, mp, mb, dt, adx, ady, tr, side);
+      substep_side<TRACE>(s, mp, mb, dt, adx, ady, tr, side, rp);
     }
     // Walker.Update + terminal flags (both upper legs and the torso)
     s.prevx = s.posx; s.prevy = s.posy;
@@ -825,6 +863,10 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArg
     t++;
   }
   store_side(s, A.st, e, side);
+#ifdef WK_REGION_PROF
+  if ((threadIdx.x & 63) == 0)
+    for (int r = 0; r < 8; r++) atomicAdd(&g_region_prof[r], (unsigned long long)rpv.acc[r]);
+#endif
   fault |= (uint32_t)pswap((float)fault);
   if (leader) {
     A.rng_t[e] = t;
@@ -940,6 +982,16 @@ hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipS
   else launch_lanes<1>(mode, P, A, s);
   return hipGetLastError();
 }
+#ifdef WK_REGION_PROF
+extern "C" int wk_region_prof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_region_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_region_prof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 hipError_t launch_env_init(const EnvParams& P, float* st, const float* dx, const uint8_t* mask,
                            int post, hipStream_t s) {
   hipLaunchKernelGGL(k_env_init, dim3((P.n_env + 255) / 256), dim3(256), 0, s, P, st, dx, mask, post);

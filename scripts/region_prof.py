@@ -1,0 +1,35 @@
+"""Per-region wave time of the side-split env-step kernel (build: make LIB=libwk_prof.so
+BUILD=build_prof EXTRA=-DWK_REGION_PROF).  python scripts/region_prof.py [walkers] [T]"""
+import ctypes as C
+import os
+import sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ppo-bipedalwalker_amd"))
+os.environ.setdefault("WK_LIB", os.path.join(ROOT, "ppo-bipedalwalker_amd", "libwk_prof.so"))
+import torch  # noqa: E402
+import wk  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+T = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+names = ["joint", "integrate", "aabb", "sat", "contact", "impulse+move", "policy", "other"]
+eng = wk.Engine(n, seed=20250905, Horizon=T, RandomizeStart=1, LanesPerWalker=2)
+lib = eng.lib
+lib.wk_region_prof.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+buf = (C.c_ulonglong * 16)()
+eng.rollout(T)
+eng.sync()
+lib.wk_region_prof(buf, 1)
+for mode in ("rollout", "physics"):
+    if mode == "rollout":
+        eng.rollout(T)
+    else:
+        act = torch.rand((T, n, 4), device="cuda") * 2 - 1
+        torch.cuda.synchronize()
+        eng.step_device(act.data_ptr(), T, None, None, None, None)
+    eng.sync()
+    lib.wk_region_prof(buf, 1)
+    tot = sum(buf[i] for i in range(8))
+    waves = n * 2 // 64
+    print(f"{mode}: total {tot / waves / (T * 50):.0f} ticks per wave-substep")
+    for i in range(8):
+        print(f"  {names[i]:14s} {100.0 * buf[i] / tot:6.2f} %  {buf[i] / waves / (T * 50):9.1f}")

@@ -340,3 +340,18 @@ def test_minibatch_gradient_mfma_vs_oracle(wk, orc, B):
     assert sk == osk
     assert cd == pytest.approx(ocd, rel=1e-4, abs=1e-6)
     assert ad == pytest.approx(oad, rel=1e-4, abs=1e-6)
+
+
+def test_fast_sqrt_rcp_exhaustive():
+    """The physics kernel's sqrt_rn / rsqrt_rn / rcp_core equal HIP's correctly rounded
+    sqrtf and division on every non-negative float (tests/cpp/fastmath_check.hip)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "ppo-bipedalwalker_amd", "build", "fastmath_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(os.path.dirname(exe)), "check"],
+                       check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 mismatches" in r.stdout
