@@ -36,12 +36,13 @@ struct wk_ctx {
   wk::EnvParams P{};
   float lp_const = 0.0f;
   // env
-  float* st = nullptr;        // [NSTATE][n]
+  float* st = nullptr;        // walker records [n][NSTATE]
   float* dxoff = nullptr;     // [n]
   int32_t* mat = nullptr;     // [n]
   uint32_t* rng_t = nullptr;  // [n]
   // params
   float* W = nullptr; float* m = nullptr; float* v = nullptr; float* grad = nullptr;
+  float* Wz = nullptr;        // W in the matrix-core operand order (wk_mfma_layout.h)
   int adam_t = 0;
   // trajectory [T][n]
   int T = 0, T_valid = 0;
@@ -267,6 +268,7 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   ALLOC(x->mat, sizeof(int32_t) * n);
   ALLOC(x->rng_t, sizeof(uint32_t) * n);
   ALLOC(x->W, sizeof(float) * wk::NPARAM);
+  ALLOC(x->Wz, sizeof(float) * wk::mfma_image_floats());
   ALLOC(x->m, sizeof(float) * wk::NPARAM);
   ALLOC(x->v, sizeof(float) * wk::NPARAM);
   ALLOC(x->grad, sizeof(float) * wk::SLAB);
@@ -298,6 +300,7 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   }
   if (wk::launch_env_init(P, x->st, x->dxoff, nullptr, 0, x->stream) != hipSuccess ||
       wk::launch_xavier(x->W, seed, x->stream) != hipSuccess ||
+      wk::launch_swizzle(x->W, x->Wz, x->stream) != hipSuccess ||
       hipStreamSynchronize(x->stream) != hipSuccess) {
     x->err = "init kernels failed";
     return fail(WK_ERR_HIP);
@@ -312,7 +315,7 @@ int wk_destroy(wk_ctx* c) {
   for (auto& e : c->pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto e : c->pool) (void)hipEventDestroy(e);
   if (c->comm) ncclCommDestroy(c->comm);
-  void* bufs[] = {c->st, c->dxoff, c->mat, c->rng_t, c->W, c->m, c->v, c->grad, c->ts, c->ta,
+  void* bufs[] = {c->st, c->dxoff, c->mat, c->rng_t, c->W, c->Wz, c->m, c->v, c->grad, c->ts, c->ta,
                   c->tlp, c->tr, c->tv, c->tret, c->tadv, c->td, c->partial, c->scratch, c->scratch2};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -362,7 +365,7 @@ static int step_impl(wk_ctx* c, const float* d_actions, int k, float* d_obs, flo
   wk::StepArgs A{};
   A.st = c->st; A.dxoff = c->dxoff; A.mat = c->mat; A.rng_t = c->rng_t;
   A.actions = d_actions; A.obs_out = d_obs; A.rew_out = d_rew; A.done_out = d_done;
-  A.fault_out = d_fault; A.W = c->W; A.lp_const = c->lp_const;
+  A.fault_out = d_fault; A.W = c->W; A.Wz = c->Wz; A.lp_const = c->lp_const;
   A.traj_s = c->ts; A.traj_a = c->ta; A.traj_lp = c->tlp; A.traj_r = c->tr; A.traj_d = c->td;
   A.traj_v = c->tv; A.t0 = 0;
   A.trace = (wk::PairTraceDev*)trace;
@@ -484,6 +487,8 @@ int wk_set_weights(wk_ctx* c, const float* p) {
   if (!c || !p) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(c->W, p, sizeof(float) * wk::NPARAM, hipMemcpyHostToDevice));
+  HIPCHK(c, wk::launch_swizzle(c->W, c->Wz, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return WK_OK;
 }
 int wk_get_adam(wk_ctx* c, float* m, float* v, int* t) {
@@ -562,7 +567,7 @@ int wk_rollout(wk_ctx* c, int horizon) {
   if (horizon > c->T) { SETERR(c, "horizon %d exceeds the configured Horizon %d", horizon, c->T); return WK_ERR_ARG; }
   wk::StepArgs A{};
   A.st = c->st; A.dxoff = c->dxoff; A.mat = c->mat; A.rng_t = c->rng_t;
-  A.W = c->W; A.lp_const = c->lp_const;
+  A.W = c->W; A.Wz = c->Wz; A.lp_const = c->lp_const;
   A.traj_s = c->ts; A.traj_a = c->ta; A.traj_lp = c->tlp; A.traj_r = c->tr; A.traj_d = c->td;
   A.traj_v = c->tv; A.t0 = 0; A.k_steps = horizon;
   {
@@ -663,7 +668,7 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
     c->adam_t += 1;
     const wk_config& k = c->cfg;
     wk::AdamArgs a;
-    a.W = c->W; a.m = c->m; a.v = c->v; a.grad = c->grad;
+    a.W = c->W; a.m = c->m; a.v = c->v; a.grad = c->grad; a.Wz = c->Wz;
     a.c1 = 1.0f - k.Beta1;
     a.c2 = 1.0f - k.Beta2;
     a.beta1 = k.Beta1;
@@ -681,6 +686,7 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
 static wk::GradArgs grad_base(wk_ctx* c) {
   wk::GradArgs g{};
   g.W = c->W;
+  g.Wz = c->Wz;
   g.std_ = c->P.std_;
   g.lp_const = c->lp_const;
   g.upper = 1.0f + c->cfg.Epsilon;

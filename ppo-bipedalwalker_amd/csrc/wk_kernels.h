@@ -34,6 +34,7 @@ struct StepArgs {
   uint8_t* done_out;         // [k][n] or null
   uint32_t* fault_out;       // [n] or null (OR-accumulated)
   const float* W;            // params (policy)
+  const float* Wz;           // params in the matrix-core operand order (wk_mfma_layout.h)
   float lp_const;            // -ln(std) - ln(sqrt(2 pi))
   // trajectory buffer (RECORD), index t*n + e
   float* traj_s; float* traj_a; float* traj_lp; float* traj_r; uint8_t* traj_d; float* traj_v;
@@ -44,6 +45,7 @@ struct StepArgs {
 
 struct GradArgs {
   const float* W;        // params
+  const float* Wz;       // the same params in the matrix-core operand order (wk_mfma_layout.h)
   const float* states;   // [P][12]
   const float* actions;  // [P][4]
   const float* logp_old; // [P][4]
@@ -64,6 +66,7 @@ struct GradArgs {
 
 struct AdamArgs {
   float* W; float* m; float* v; const float* grad;
+  float* Wz;  // operand-order image kept in step with W (or null)
   float c1, c2, beta1, beta2, bc1, bc2, alpha, eps;
 };
 
@@ -80,6 +83,8 @@ hipError_t launch_returns(int n, int T, int use_gae, float gamma, float lambda, 
                           const float* v, const uint8_t* d, float* ret, float* adv, hipStream_t s);
 hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t s);
 hipError_t launch_ppo_grad_mfma(const GradArgs& g, int nblocks, hipStream_t s);
+hipError_t launch_swizzle(const float* W, float* Wz, hipStream_t s);
+int mfma_image_floats();
 int ppo_grad_mfma_blocks(int samples);
 hipError_t launch_grad_reduce(const float* partial, int nblocks, float* part2, float* grad,
                               hipStream_t s);

@@ -1,0 +1,56 @@
+// wk_mfma_layout.h -- the matrix-core gradient kernel's weight image (wk_ppo_mfma.hip).
+//
+// The policy parameters (wk_common.h OFF_*) are kept a second time in HBM in the exact
+// order the v_mfma_f32_16x16x4_f32 A operands read them (lane l = 16 g + n holds A[n][g]),
+// so each gradient block stages them into LDS with a straight 16-byte copy.  The image is
+// rewritten by every Adam step (k_adam scatters each updated parameter) and by the
+// initialisation / set-weights paths (k_swizzle).
+#pragma once
+#include "wk_common.h"
+
+namespace wk {
+namespace mf {
+enum : int {
+  AW1F = 0,              // [Mt 4][t 3][lane 64]        W1[16Mt + n][4t + g]
+  CW1F = AW1F + 768,     // critic W1, same order
+  W2F = CW1F + 768,      // [Mt 4][Mp 4][lane 64][r 4]  W2[16Mt + n][16Mp + 4g + r]
+  W2B = W2F + 4096,      // [Mk 4][Mj 4][lane 64][r 4]  W2[16Mj + 4g + r][16Mk + n]
+  W3 = W2B + 4096,       // [4][64]
+  WC2 = W3 + 256,        // [64]
+  BA1 = WC2 + 64, BA2 = BA1 + 64, BC1 = BA2 + 64, BA3 = BC1 + 64, BC2 = BA3 + 4,
+  WEND = BC2 + 4         // 10,248 floats
+};
+static_assert(WEND % 4 == 0, "16-byte copies");
+}  // namespace mf
+
+// write parameter p (value v) to its image position(s)
+__device__ inline void mf_scatter_param(float* __restrict__ Wz, int p, float v) {
+  using namespace mf;
+  if (p < OFF_C_B1 || (p >= OFF_A_W1 && p < OFF_A_B1)) {  // W1 (critic / actor) [64][12]
+    const bool critic = p < OFF_C_B1;
+    const int q = p - (critic ? OFF_C_W1 : OFF_A_W1);
+    const int j = q / 12, k = q % 12;
+    Wz[(critic ? CW1F : AW1F) + ((j >> 4) * 3 + (k >> 2)) * 64 + 16 * (k & 3) + (j & 15)] = v;
+  } else if (p < OFF_C_W2) {
+    Wz[BC1 + p - OFF_C_B1] = v;
+  } else if (p < OFF_C_B2) {
+    Wz[WC2 + p - OFF_C_W2] = v;
+  } else if (p < OFF_A_W1) {
+    Wz[BC2] = v;
+  } else if (p < OFF_A_W2) {
+    Wz[BA1 + p - OFF_A_B1] = v;
+  } else if (p < OFF_A_B2) {  // W2 [64 j][64 k], both operand orders
+    const int q = p - OFF_A_W2;
+    const int j = q >> 6, k = q & 63;
+    Wz[W2F + (((j >> 4) * 4 + (k >> 4)) * 64 + 16 * ((k & 15) >> 2) + (j & 15)) * 4 + (k & 3)] = v;
+    Wz[W2B + (((k >> 4) * 4 + (j >> 4)) * 64 + 16 * ((j & 15) >> 2) + (k & 15)) * 4 + (j & 3)] = v;
+  } else if (p < OFF_A_W3) {
+    Wz[BA2 + p - OFF_A_B2] = v;
+  } else if (p < OFF_A_B3) {
+    Wz[W3 + p - OFF_A_W3] = v;
+  } else {
+    Wz[BA3 + p - OFF_A_B3] = v;
+  }
+}
+
+}  // namespace wk

@@ -18,6 +18,7 @@
 #include "wk_common.h"
 #include "wk_device.h"
 #include "wk_kernels.h"
+#include "wk_mfma_layout.h"
 
 #ifndef WK_ENV_WAVES
 #define WK_ENV_WAVES 2
@@ -753,13 +754,133 @@ DEV bool side_finite(const SideState& s) {
   return acc == 0.0f;
 }
 
+// PPOAgent.SampleActions / GetValueEstimate forward passes (NeuralNetwork.FeedForward,
+// DenseLayer.cs:82-98) for the 32 walkers of a wave on the matrix cores, with the layouts
+// of wk_ppo_mfma.hip: observations staged through LDS into v_mfma_f32_16x16x4_f32 B
+// operands (walkers on n, two 16-walker tiles), W1 / W2 A operands streamed from the
+// operand-order image (wk_mfma_layout.h, L2-resident), layer 2 chained on layer 1's D
+// registers, and the 64-long output rows (actor W3, critic Wc2) on the VALU summed over
+// the four lane groups.  fp32 throughout; only the association of the k-sums differs
+// from the sequential reference (parity tests: rtol 1e-5).
+typedef float pf4 __attribute__((ext_vector_type(4)));
+DEV pf4 pmfma(float a, float b, pf4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+DEV float plrelu(float z) { return net_maxf(0.2f * z, z); }
+
+DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], int side,
+                     float* __restrict__ pl, float z3[4], float& value) {
+  using namespace mf;
+  const int lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4, wl = lane >> 1;
+  float* tile = pl;          // [32 walkers][16]: 12 observations
+  float* outs = pl + 512;    // [32 walkers][8]: z3[0..3], critic output
+  if (side == 0) {
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const pf4 v = {obs[4 * q], obs[4 * q + 1], obs[4 * q + 2], obs[4 * q + 3]};
+      *(pf4*)(tile + wl * 16 + 4 * q) = v;
+    }
+  }
+  wave_lds_sync();
+  float sB[2][3];
+#pragma unroll
+  for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+    for (int t = 0; t < 3; t++) sB[nt][t] = tile[(16 * nt + n) * 16 + 4 * t + g];
+  const pf4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+  pf4 h1[2][4];
+  float pv[2] = {0.0f, 0.0f};
+#pragma unroll
+  for (int Mt = 0; Mt < 4; Mt++) {
+    float wa[3], wc[3];
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+      wa[t] = Wz[AW1F + (Mt * 3 + t) * 64 + lane];
+      wc[t] = Wz[CW1F + (Mt * 3 + t) * 64 + lane];
+    }
+    const pf4 ba = *(const pf4*)(Wz + BA1 + 16 * Mt + 4 * g);
+    const pf4 bc = *(const pf4*)(Wz + BC1 + 16 * Mt + 4 * g);
+    const pf4 w2c = *(const pf4*)(Wz + WC2 + 16 * Mt + 4 * g);
+#pragma unroll
+    for (int nt = 0; nt < 2; nt++) {
+      pf4 acc = z4, accc = z4;
+#pragma unroll
+      for (int t = 0; t < 3; t++) {
+        acc = pmfma(wa[t], sB[nt][t], acc);
+        accc = pmfma(wc[t], sB[nt][t], accc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        h1[nt][Mt][r] = plrelu(acc[r] + ba[r]);
+        pv[nt] = pv[nt] + w2c[r] * plrelu(accc[r] + bc[r]);
+      }
+    }
+  }
+  float p3[2][4];
+#pragma unroll
+  for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+    for (int d = 0; d < 4; d++) p3[nt][d] = 0.0f;
+#pragma unroll 1
+  for (int Mt = 0; Mt < 4; Mt++) {  // not unrolled: keeps one Mt's weights in flight
+    pf4 acc[2] = {z4, z4};
+#pragma unroll
+    for (int Mp = 0; Mp < 4; Mp++) {
+      const pf4 w = *(const pf4*)(Wz + W2F + ((Mt * 4 + Mp) * 64 + lane) * 4);
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) acc[nt] = pmfma(w[r], h1[nt][Mp][r], acc[nt]);
+    }
+    const pf4 b2 = *(const pf4*)(Wz + BA2 + 16 * Mt + 4 * g);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int k = 16 * Mt + 4 * g + r;
+#pragma unroll
+      for (int nt = 0; nt < 2; nt++) {
+        const float h2 = plrelu(acc[nt][r] + b2[r]);
+#pragma unroll
+        for (int d = 0; d < 4; d++) p3[nt][d] = p3[nt][d] + Wz[W3 + d * 64 + k] * h2;
+      }
+    }
+  }
+#pragma unroll
+  for (int nt = 0; nt < 2; nt++) {
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      p3[nt][d] = p3[nt][d] + __shfl_xor(p3[nt][d], 16);
+      p3[nt][d] = p3[nt][d] + __shfl_xor(p3[nt][d], 32);
+    }
+    pv[nt] = pv[nt] + __shfl_xor(pv[nt], 16);
+    pv[nt] = pv[nt] + __shfl_xor(pv[nt], 32);
+  }
+  wave_lds_sync();  // the tile reads above are done before the outputs reuse LDS
+  if (g == 0) {
+#pragma unroll
+    for (int nt = 0; nt < 2; nt++) {
+      const pf4 v = {p3[nt][0], p3[nt][1], p3[nt][2], p3[nt][3]};
+      *(pf4*)(outs + (16 * nt + n) * 8) = v;
+      outs[(16 * nt + n) * 8 + 4] = pv[nt];
+    }
+  }
+  wave_lds_sync();
+  const pf4 b3 = *(const pf4*)(Wz + BA3);
+  const pf4 o = *(const pf4*)(outs + wl * 8);
+#pragma unroll
+  for (int d = 0; d < 4; d++) z3[d] = o[d] + b3[d];
+  value = outs[wl * 8 + 4] + Wz[BC2];
+  wave_lds_sync();  // outputs read before the next env-step rewrites the tile
+}
+
 template <bool POLICY, bool RECORD, bool TRACE>
 __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArgs A) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int e = tid >> 1, side = tid & 1;
+  const int side = tid & 1;
   const int n = P.n_env;
-  if (e >= n) return;  // both lanes of a pair exit together
-  const bool leader = side == 0;
+  // a partial last wave keeps every lane (the policy's MFMAs need the whole wave):
+  // out-of-range pairs replay walker n-1 and never store
+  const bool active = (tid >> 1) < n;
+  const int e = active ? (tid >> 1) : n - 1;
+  const bool leader = side == 0 && active;
+  __shared__ float pol_lds[POLICY ? 512 + 256 : 1];
   SideState s;
   load_side(s, A.st, e, side);
   const float dx = A.dxoff[e];
@@ -785,11 +906,11 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArg
     rp_mark(rp, RP_OTHER);
     if (POLICY) {
       get_obs_side(s, side, obs);
-      float mean[4];
-      actor_mean(A.W, obs, mean);
+      float z3[4], mean[4], v;
+      policy_mfma(A.Wz, obs, side, pol_lds, z3, v);
+#pragma unroll
+      for (int d = 0; d < 4; d++) mean[d] = tanhf(z3[d]);
       sample_actions(P, A.lp_const, gid, t, mean, a, lp);
-      float v = 0.0f;
-      if (RECORD) v = critic_value(A.W, obs);
       if (RECORD && leader) {
         const size_t idx = (size_t)(A.t0 + k) * n + e;
 #pragma unroll
@@ -815,7 +936,7 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArg
     }
 #pragma unroll 1
     for (int it = 0; it < P.iterations; it++) {
-      PairTraceDev* tr = TRACE ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
+      PairTraceDev* tr = (TRACE && active) ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
       substep_side<TRACE>(s, mp, mb, dt, adx, ady, tr, side, rp);
     }
     // Walker.Update + terminal flags (both upper legs and the torso)
@@ -862,7 +983,7 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArg
     }
     t++;
   }
-  store_side(s, A.st, e, side);
+  if (active) store_side(s, A.st, e, side);
 #ifdef WK_REGION_PROF
   if ((threadIdx.x & 63) == 0)
     for (int r = 0; r < 8; r++) atomicAdd(&g_region_prof[r], (unsigned long long)rpv.acc[r]);

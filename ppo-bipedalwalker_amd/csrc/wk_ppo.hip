@@ -14,6 +14,7 @@
 // reproduces the reference's sequential accumulation exactly.
 #include "wk_common.h"
 #include "wk_kernels.h"
+#include "wk_mfma_layout.h"
 
 namespace wk {
 
@@ -290,7 +291,9 @@ __global__ void k_adam(AdamArgs a) {
   float mh = m / a.bc1;
   float vh = v / a.bc2;
   float den = sqrtf(vh) + a.eps;
-  a.W[p] = a.W[p] - ((mh / den) * a.alpha);
+  const float w = a.W[p] - ((mh / den) * a.alpha);
+  a.W[p] = w;
+  if (a.Wz) mf_scatter_param(a.Wz, p, w);
 }
 
 // Normalize (PPOAgent.cs:461-472): LINQ Average/Sum accumulate in double

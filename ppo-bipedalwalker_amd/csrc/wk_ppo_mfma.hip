@@ -27,6 +27,7 @@
 // slabs for the ordered reduction (bit-reproducible, no atomics).
 #include "wk_common.h"
 #include "wk_kernels.h"
+#include "wk_mfma_layout.h"
 
 namespace wk {
 
@@ -35,24 +36,16 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 namespace mf {
 enum : int {
-  AW1F = 0,              // [Mt 4][t 3][lane 64]        W1[16Mt + n][4t + g]
-  CW1F = AW1F + 768,     // critic W1, same order
-  W2F = CW1F + 768,      // [Mt 4][Mp 4][lane 64][r 4]  W2[16Mt + n][16Mp + 4g + r]
-  W2B = W2F + 4096,      // [Mk 4][Mj 4][lane 64][r 4]  W2[16Mj + 4g + r][16Mk + n]
-  W3 = W2B + 4096,       // [4][64]
-  WC2 = W3 + 256,        // [64]
-  BA1 = WC2 + 64, BA2 = BA1 + 64, BC1 = BA2 + 64, BA3 = BC1 + 64, BC2 = BA3 + 4,
-  WEND = BC2 + 4,
   RS = 80,               // row stride of a [16 samples][64] tile
   C_H1 = 0, C_HC1 = C_H1 + 16 * RS, C_H2 = C_HC1 + 16 * RS, C_G2 = C_H2 + 16 * RS,
   C_SX = C_G2 + 16 * RS,  // [16][16]: 12 features, 1.0 (bias column), 0, 0, 0
   C_G3 = C_SX + 256,      // [16][16]: gz3 (4 dims), dV, zeros
   CHUNK = C_G3 + 256,
   C_G1 = C_H2, C_GC1 = C_HC1,  // backward tiles reuse the forward ones
-  WAVES = 4
+  WAVES = 4,
+  LDS_FLOATS = WEND + WAVES * CHUNK
 };
-static_assert(WEND % 4 == 0, "16-byte aligned chunk tiles");
-static_assert(WAVES * CHUNK >= SLAB, "slab fits the chunk tiles");
+static_assert(LDS_FLOATS >= WAVES * SLAB, "the epilogue's per-wave slabs fit");
 }  // namespace mf
 
 DEV float mf_lrelu(float z) {  // ActivationLayer LeakyReLU(0.2): Math.Max(0.2 z, z)
@@ -83,28 +76,8 @@ void k_ppo_grad_mfma(GradArgs ga) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, g = lane >> 4;
 
-  // ---- stage the pre-swizzled weights ----
-  const float* W = ga.W;
-  for (int e = tid; e < 768; e += 64 * WAVES) {
-    const int Mt = e / 192, t = (e / 64) % 3, l = e & 63;
-    const int m = 16 * Mt + (l & 15), k = 4 * t + (l >> 4);
-    lds[AW1F + e] = W[OFF_A_W1 + m * 12 + k];
-    lds[CW1F + e] = W[OFF_C_W1 + m * 12 + k];
-  }
-  for (int e = tid; e < 4096; e += 64 * WAVES) {
-    const int A = e >> 10, B = (e >> 8) & 3, l = (e >> 2) & 63, r = e & 3;
-    lds[W2F + e] = W[OFF_A_W2 + (16 * A + (l & 15)) * 64 + 16 * B + 4 * (l >> 4) + r];
-    lds[W2B + e] = W[OFF_A_W2 + (16 * B + 4 * (l >> 4) + r) * 64 + 16 * A + (l & 15)];
-  }
-  for (int e = tid; e < 256; e += 64 * WAVES) lds[W3 + e] = W[OFF_A_W3 + e];
-  for (int e = tid; e < 64; e += 64 * WAVES) {
-    lds[WC2 + e] = W[OFF_C_W2 + e];
-    lds[BA1 + e] = W[OFF_A_B1 + e];
-    lds[BA2 + e] = W[OFF_A_B2 + e];
-    lds[BC1 + e] = W[OFF_C_B1 + e];
-  }
-  if (tid < 4) lds[BA3 + tid] = W[OFF_A_B3 + tid];
-  if (tid == 0) lds[BC2] = W[OFF_C_B2];
+  // ---- stage the weight image (already in operand order, wk_mfma_layout.h) ----
+  for (int e = tid; e < WEND / 4; e += 64 * WAVES) ((f4*)lds)[e] = ((const f4*)ga.Wz)[e];
   float* cb = lds + WEND + wave * CHUNK;
   for (int e = lane; e < 256; e += 64) cb[C_G3 + e] = 0.0f;
   __syncthreads();
@@ -128,20 +101,30 @@ void k_ppo_grad_mfma(GradArgs ga) {
   const float b3g = lds[BA3 + g], bc2 = lds[BC2];
   const int nchunks = (ga.samples + 15) / 16;
   const int nw = gridDim.x * WAVES;
-#pragma unroll 1
-  for (int c = blockIdx.x * WAVES + wave; c < nchunks; c += nw) {
-    // ---- gather (CreateBatches, PPOAgent.cs:512-533) ----
+  // gather (CreateBatches, PPOAgent.cs:512-533), one chunk ahead of the math
+  struct Smp { f4 sv; float act, lpo, ret, adv; };
+  auto gather = [&](int c) {
+    Smp m;
     const int pos = c * 16 + n;
-    const bool valid = pos < ga.samples;
-    uint32_t idx = ga.base + (uint32_t)(valid ? pos : 0);
+    uint32_t idx = ga.base + (uint32_t)(pos < ga.samples ? pos : 0);
     if (ga.use_perm) idx = perm_apply(idx, ga.pk);
-    f4 sv = {1.0f, 0.0f, 0.0f, 0.0f};  // lane group 3: the bias column
-    if (g < 3) sv = *(const f4*)(ga.states + (size_t)idx * 12 + 4 * g);
-    *(f4*)(cb + C_SX + n * 16 + 4 * g) = sv;
-    const float act = ga.actions[(size_t)idx * 4 + g];
-    const float lpo = ga.logp_old[(size_t)idx * 4 + g];
-    const float ret = ga.returns[idx];
-    const float adv = ga.adv[idx];
+    m.sv = f4{1.0f, 0.0f, 0.0f, 0.0f};  // lane group 3: the bias column
+    if (g < 3) m.sv = *(const f4*)(ga.states + (size_t)idx * 12 + 4 * g);
+    m.act = ga.actions[(size_t)idx * 4 + g];
+    m.lpo = ga.logp_old[(size_t)idx * 4 + g];
+    m.ret = ga.returns[idx];
+    m.adv = ga.adv[idx];
+    return m;
+  };
+  int c = blockIdx.x * WAVES + wave;
+  Smp nxt = gather(c < nchunks ? c : 0);
+#pragma unroll 1
+  for (; c < nchunks; c += nw) {
+    const Smp cur = nxt;
+    if (c + nw < nchunks) nxt = gather(c + nw);
+    const bool valid = c * 16 + n < ga.samples;
+    const float act = cur.act, lpo = cur.lpo, ret = cur.ret, adv = cur.adv;
+    *(f4*)(cb + C_SX + n * 16 + 4 * g) = cur.sv;
     wave_sync();
 
     // ---- layer 1, actor and critic ----
@@ -339,56 +322,68 @@ void k_ppo_grad_mfma(GradArgs ga) {
   diagA = row_sum16(diagA);
   skipped = row_sum16(skipped);
 
-  // ---- fold the waves into the block slab in wave order ----
-  __syncthreads();
-  float* slab = lds + WEND;
-  for (int i = tid; i < SLAB; i += 64 * WAVES) slab[i] = 0.0f;
-  __syncthreads();
-#pragma unroll 1
-  for (int w = 0; w < WAVES; w++) {
-    if (w == wave) {
+  // ---- each wave writes its slab, then the block sums them in wave order ----
+  __syncthreads();  // every wave is done with the weights and tiles
+  float* slab = lds + wave * SLAB;
+  for (int i = lane; i < SLAB; i += 64) slab[i] = 0.0f;
+  wave_sync();
 #pragma unroll
-      for (int Mj = 0; Mj < 4; Mj++)
+  for (int Mj = 0; Mj < 4; Mj++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int j = 16 * Mj + 4 * g + r;
+    for (int r = 0; r < 4; r++) {
+      const int j = 16 * Mj + 4 * g + r;
 #pragma unroll
-          for (int Nk = 0; Nk < 4; Nk++) slab[OFF_A_W2 + j * 64 + 16 * Nk + n] += a2[Mj][Nk][r];
-          if (n < 12) {
-            slab[OFF_A_W1 + j * 12 + n] += a1[Mj][r];
-            slab[OFF_C_W1 + j * 12 + n] += a1c[Mj][r];
-          } else if (n == 12) {
-            slab[OFF_A_B1 + j] += a1[Mj][r];
-            slab[OFF_C_B1 + j] += a1c[Mj][r];
-          }
-        }
-#pragma unroll
-      for (int Nt = 0; Nt < 4; Nt++) {
-        if (g == 0) {
-#pragma unroll
-          for (int r = 0; r < 4; r++) slab[OFF_A_W3 + r * 64 + 16 * Nt + n] += a3[Nt][r];
-        } else if (g == 1) {
-          slab[OFF_C_W2 + 16 * Nt + n] += a3[Nt + 4][0];
-        }
-      }
-      if (n == 0) {
-#pragma unroll
-        for (int Mt = 0; Mt < 4; Mt++)
-#pragma unroll
-          for (int r = 0; r < 4; r++) slab[OFF_A_B2 + 16 * Mt + 4 * g + r] += db2[Mt * 4 + r];
-        slab[OFF_A_B3 + g] += db3;
-        if (g == 0) {
-          slab[OFF_C_B2] += dbc2;
-          slab[NPARAM] += diagC;
-          slab[NPARAM + 1] += diagA;
-          slab[NPARAM + 2] += skipped;
-        }
+      for (int Nk = 0; Nk < 4; Nk++) slab[OFF_A_W2 + j * 64 + 16 * Nk + n] = a2[Mj][Nk][r];
+      if (n < 12) {
+        slab[OFF_A_W1 + j * 12 + n] = a1[Mj][r];
+        slab[OFF_C_W1 + j * 12 + n] = a1c[Mj][r];
+      } else if (n == 12) {
+        slab[OFF_A_B1 + j] = a1[Mj][r];
+        slab[OFF_C_B1 + j] = a1c[Mj][r];
       }
     }
-    __syncthreads();
+#pragma unroll
+  for (int Nt = 0; Nt < 4; Nt++) {
+    if (g == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) slab[OFF_A_W3 + r * 64 + 16 * Nt + n] = a3[Nt][r];
+    } else if (g == 1) {
+      slab[OFF_C_W2 + 16 * Nt + n] = a3[Nt + 4][0];
+    }
   }
+  if (n == 0) {
+#pragma unroll
+    for (int Mt = 0; Mt < 4; Mt++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) slab[OFF_A_B2 + 16 * Mt + 4 * g + r] = db2[Mt * 4 + r];
+    slab[OFF_A_B3 + g] = db3;
+    if (g == 0) {
+      slab[OFF_C_B2] = dbc2;
+      slab[NPARAM] = diagC;
+      slab[NPARAM + 1] = diagA;
+      slab[NPARAM + 2] = skipped;
+    }
+  }
+  __syncthreads();
   float* out = ga.partial + (size_t)blockIdx.x * SLAB;
-  for (int i = tid; i < SLAB; i += 64 * WAVES) out[i] = slab[i];
+  for (int i = tid; i < SLAB; i += 64 * WAVES) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int w = 0; w < WAVES; w++) acc = acc + lds[w * SLAB + i];
+    out[i] = acc;
+  }
+}
+
+// the weight image from the flat parameters (initialisation, wk_set_weights)
+__global__ void k_swizzle(const float* __restrict__ W, float* __restrict__ Wz) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < NPARAM) mf_scatter_param(Wz, p, W[p]);
+}
+
+int mfma_image_floats() { return mf::WEND; }
+hipError_t launch_swizzle(const float* W, float* Wz, hipStream_t s) {
+  hipLaunchKernelGGL(k_swizzle, dim3((NPARAM + 255) / 256), dim3(256), 0, s, W, Wz);
+  return hipGetLastError();
 }
 
 int ppo_grad_mfma_blocks(int samples) {
@@ -398,7 +393,7 @@ int ppo_grad_mfma_blocks(int samples) {
 }
 
 hipError_t launch_ppo_grad_mfma(const GradArgs& g, int nblocks, hipStream_t s) {
-  const size_t lds = sizeof(float) * (mf::WEND + mf::WAVES * mf::CHUNK);
+  const size_t lds = sizeof(float) * mf::LDS_FLOATS;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)k_ppo_grad_mfma,

@@ -296,20 +296,34 @@ def test_step_device_pointers(wk):
 
 
 def test_mappings_agree_at_scale(wk):
-    """Size-independent property at the bench's per-GPU size: the three physics mappings
-    (and the fused policy) produce bit-identical rollouts, trajectories and states."""
+    """Size-independent properties at the bench's per-GPU size (65,536 walkers): the
+    three physics mappings step bit-identically on the same actions, and a policy
+    rollout of the default (side-split, matrix-core policy) mapping replays exactly
+    through the one-lane mapping's physics."""
     n, T = 65536, 4
+    rng = np.random.default_rng(9)
+    acts = rng.uniform(-1.2, 1.2, (T, n, 4)).astype(F)
     outs = []
     for lanes in LANES:
         eng = wk.Engine(n, seed=SEED, Horizon=T, RandomizeStart=1, RandomizeMaterial=1,
                         LanesPerWalker=lanes)
-        eng.rollout(T)
-        tr = eng.get_trajectory(T)
-        outs.append((eng.get_state(), tr["states"], tr["rewards"], tr["dones"], tr["actions"]))
+        obs, rew, done, fault = eng.step(acts, k=T)
+        outs.append((eng.get_state(), obs, rew, done))
         eng.close()
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             np.testing.assert_array_equal(a, b)
+    roll = wk.Engine(n, seed=SEED, Horizon=T, RandomizeStart=1, RandomizeMaterial=1,
+                     LanesPerWalker=2)
+    replay = wk.Engine(n, seed=SEED, Horizon=T, RandomizeStart=1, RandomizeMaterial=1,
+                       LanesPerWalker=1)
+    roll.rollout(T)
+    tr = roll.get_trajectory(T)
+    obs, rew, done, _ = replay.step(tr["actions"], k=T)
+    np.testing.assert_array_equal(rew, tr["rewards"])
+    np.testing.assert_array_equal(done, tr["dones"])
+    np.testing.assert_array_equal(obs[:-1], tr["states"][1:])
+    np.testing.assert_array_equal(replay.get_state(), roll.get_state())
 
 
 def test_invalid_lanes_rejected(wk):
