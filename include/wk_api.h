@@ -167,6 +167,7 @@ typedef struct wk_profile {
   double adam_ms;      int64_t adam_launches;
   double allreduce_ms; int64_t allreduce_calls;
   double returns_ms;   int64_t returns_launches;
+  double update_ms;    int64_t update_calls;     /* whole wk_ppo_update calls */
 } wk_profile;
 
 void wk_config_defaults(wk_config* cfg);
@@ -233,6 +234,9 @@ int wk_comm_init(wk_ctx* ctx, int rank, int nranks, const uint8_t* unique_id);
 int wk_allreduce_test(wk_ctx* ctx, float* host_buf, int n); /* sum in place (tests) */
 
 /* profiling */
+/* level 0 off; 1: HIP events around each rollout / returns pass / whole PPO update (cheap
+ * enough inside a timed loop); 2: also around every gradient / reduce / all-reduce / Adam
+ * launch of the update */
 int wk_profile_enable(wk_ctx* ctx, int on);
 int wk_profile_get(wk_ctx* ctx, wk_profile* out);
 int wk_profile_reset(wk_ctx* ctx);

@@ -24,7 +24,9 @@ static const char* kCriticDefault = "Input |64| (LeakyReLU) |1| Output";
 static const char* kActorDefault = "Input |64| (LeakyReLU) |64| (LeakyReLU) |4| (TanH) Output";
 static thread_local std::string g_create_error;
 
-enum ProfKind { PK_PHYS = 0, PK_GRAD, PK_REDUCE, PK_ADAM, PK_ALLRED, PK_RET, PK_N };
+// level 1: one event pair per rollout / returns / whole PPO update (cheap enough for a
+// timed loop); level 2 adds one per gradient / reduce / all-reduce / Adam launch
+enum ProfKind { PK_PHYS = 0, PK_GRAD, PK_REDUCE, PK_ADAM, PK_ALLRED, PK_RET, PK_UPDATE, PK_N };
 
 struct wk_ctx {
   wk_config cfg;
@@ -57,7 +59,7 @@ struct wk_ctx {
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
   // profiling
-  bool prof = false;
+  int prof = 0;  // profile level
   struct Ev { int kind; hipEvent_t a, b; int64_t units; };
   std::vector<Ev> pending;
   std::vector<hipEvent_t> pool;
@@ -95,14 +97,16 @@ static hipEvent_t ev_get(wk_ctx* c) {
 
 struct ProfScope {
   wk_ctx* c; int kind; int64_t units; hipEvent_t a = nullptr, b = nullptr;
-  ProfScope(wk_ctx* c_, int k, int64_t u = 0) : c(c_), kind(k), units(u) {
-    if (c->prof) {
+  bool on;
+  ProfScope(wk_ctx* c_, int k, int64_t u = 0, int level = 1)
+      : c(c_), kind(k), units(u), on(c_->prof >= level) {
+    if (on) {
       a = ev_get(c); b = ev_get(c);
       if (a) (void)hipEventRecord(a, c->stream);
     }
   }
   ~ProfScope() {
-    if (c->prof && a && b) {
+    if (on && a && b) {
       (void)hipEventRecord(b, c->stream);
       c->pending.push_back({kind, a, b, units});
     }
@@ -649,17 +653,17 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   }
   g.partial = c->partial;
   {
-    ProfScope ps(c, PK_GRAD);
+    ProfScope ps(c, PK_GRAD, 0, 2);
     HIPCHK(c, wpb == 0 ? wk::launch_ppo_grad_mfma(g, nblocks, c->stream)
                        : wk::launch_ppo_grad(g, wpb, nblocks, c->stream));
   }
   {
-    ProfScope ps(c, PK_REDUCE);
+    ProfScope ps(c, PK_REDUCE, 0, 2);
     HIPCHK(c, wk::launch_grad_reduce(c->partial, nblocks, c->partial + (size_t)nblocks * wk::SLAB,
                                      c->grad, c->stream));
   }
   if (c->comm && c->nranks > 1) {
-    ProfScope ps(c, PK_ALLRED);
+    ProfScope ps(c, PK_ALLRED, 0, 2);
     ncclResult_t r = ncclAllReduce(c->grad, c->grad, wk::SLAB, ncclFloat, ncclSum,
                                    c->comm, c->stream);
     if (r != ncclSuccess) { SETERR(c, "ncclAllReduce: %s", ncclGetErrorString(r)); return WK_ERR_COMM; }
@@ -677,7 +681,7 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
     a.bc2 = (float)(1.0 - pow((double)k.Beta2, (double)c->adam_t));
     a.alpha = k.Alpha;
     a.eps = k.AdamEpsilon;
-    ProfScope ps(c, PK_ADAM);
+    ProfScope ps(c, PK_ADAM, 0, 2);
     HIPCHK(c, wk::launch_adam(a, c->stream));
   }
   return WK_OK;
@@ -694,9 +698,25 @@ static wk::GradArgs grad_base(wk_ctx* c) {
   return g;
 }
 
+static int ppo_update_impl(wk_ctx* c, const wk_ppo_args* args);
 int wk_ppo_update(wk_ctx* c, const wk_ppo_args* args, float* critic_diag, float* actor_diag) {
   if (!c) return WK_ERR_ARG;
   if (c->T_valid <= 0) { SETERR(c, "wk_ppo_update before wk_rollout / wk_set_trajectory"); return WK_ERR_STATE; }
+  {
+    ProfScope ps(c, PK_UPDATE);
+    int r = ppo_update_impl(c, args);
+    if (r) return r;
+  }
+  if (!critic_diag && !actor_diag) return WK_OK;  // stays asynchronous on the stream
+  float diag[3] = {0, 0, 0};
+  HIPCHK(c, hipMemcpyAsync(diag, c->grad + wk::NPARAM, sizeof(diag), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (critic_diag) *critic_diag = diag[0];
+  if (actor_diag) *actor_diag = diag[1];
+  return WK_OK;
+}
+
+static int ppo_update_impl(wk_ctx* c, const wk_ppo_args* args) {
   if (!c->returns_valid) {
     int r = returns_impl(c);
     if (r) return r;
@@ -726,11 +746,6 @@ int wk_ppo_update(wk_ctx* c, const wk_ppo_args* args, float* critic_diag, float*
       if (r) return r;
     }
   }
-  float diag[3] = {0, 0, 0};
-  HIPCHK(c, hipMemcpyAsync(diag, c->grad + wk::NPARAM, sizeof(diag), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (critic_diag) *critic_diag = diag[0];
-  if (actor_diag) *actor_diag = diag[1];
   return WK_OK;
 }
 
@@ -821,7 +836,7 @@ int wk_allreduce_test(wk_ctx* c, float* host_buf, int n) {
 
 int wk_profile_enable(wk_ctx* c, int on) {
   if (!c) return WK_ERR_ARG;
-  c->prof = on != 0;
+  c->prof = on < 0 ? 0 : (on > 2 ? 2 : on);
   return WK_OK;
 }
 
@@ -845,6 +860,7 @@ int wk_profile_get(wk_ctx* c, wk_profile* o) {
   o->adam_ms = c->prof_ms[PK_ADAM]; o->adam_launches = c->prof_cnt[PK_ADAM];
   o->allreduce_ms = c->prof_ms[PK_ALLRED]; o->allreduce_calls = c->prof_cnt[PK_ALLRED];
   o->returns_ms = c->prof_ms[PK_RET]; o->returns_launches = c->prof_cnt[PK_RET];
+  o->update_ms = c->prof_ms[PK_UPDATE]; o->update_calls = c->prof_cnt[PK_UPDATE];
   return WK_OK;
 }
 

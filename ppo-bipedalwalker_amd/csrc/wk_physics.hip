@@ -764,7 +764,7 @@ DEV bool side_finite(const SideState& s) {
 // from the sequential reference (parity tests: rtol 1e-5).
 typedef float pf4 __attribute__((ext_vector_type(4)));
 DEV pf4 pmfma(float a, float b, pf4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
-DEV float plrelu(float z) { return net_maxf(0.2f * z, z); }
+DEV float plrelu(float z) { return z < 0.0f ? 0.2f * z : z; }  // == Math.Max(0.2 z, z), see mf_lrelu
 
 DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], int side,
                      float* __restrict__ pl, float z3[4], float& value) {

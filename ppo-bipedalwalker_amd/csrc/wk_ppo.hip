@@ -24,7 +24,7 @@ DEV float net_maxf_(float x, float y) {
   if (x != y) { if (!__builtin_isnan(x)) return y < x ? x : y; return x; }
   return __builtin_signbit(y) ? x : y;
 }
-DEV float lrelu(float z) { return net_maxf_(0.2f * z, z); }
+DEV float lrelu(float z) { return z < 0.0f ? 0.2f * z : z; }  // == Math.Max(0.2 z, z) incl. -0, NaN
 DEV float dlrelu(float z) { return z < 0.0f ? 0.2f : 1.0f; }
 
 // LDS weight image (floats)

@@ -48,11 +48,9 @@ enum : int {
 static_assert(LDS_FLOATS >= WAVES * SLAB, "the epilogue's per-wave slabs fit");
 }  // namespace mf
 
-DEV float mf_lrelu(float z) {  // ActivationLayer LeakyReLU(0.2): Math.Max(0.2 z, z)
-  const float a = 0.2f * z;
-  if (a != z) { if (!__builtin_isnan(a)) return z < a ? a : z; return a; }
-  return __builtin_signbit(z) ? a : z;
-}
+// ActivationLayer LeakyReLU(0.2) = Math.Max(0.2 z, z): z for z >= 0 (and -0: Max keeps
+// the equal-valued 0.2 * -0 = -0), 0.2 z below, NaN through -- a select, no branches
+DEV float mf_lrelu(float z) { return z < 0.0f ? 0.2f * z : z; }
 DEV float mf_dlrelu(float z) { return z < 0.0f ? 0.2f : 1.0f; }
 DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -99,6 +97,24 @@ void k_ppo_grad_mfma(GradArgs ga) {
   float db3 = 0.0f, dbc2 = 0.0f, diagC = 0.0f, diagA = 0.0f, skipped = 0.0f;
 
   const float b3g = lds[BA3 + g], bc2 = lds[BC2];
+  // per-lane constants: this lane's rows of W1 / Wc1 (A operands), biases, W3 and Wc2
+  // entries of its 16 neurons 16 Mt + 4 g + r
+  float wa1[4][3], wc1[4][3];
+  f4 ba1[4], bc1[4], ba2[4], wc2[4], w3[4][4];
+#pragma unroll
+  for (int Mt = 0; Mt < 4; Mt++) {
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+      wa1[Mt][t] = lds[AW1F + (Mt * 3 + t) * 64 + lane];
+      wc1[Mt][t] = lds[CW1F + (Mt * 3 + t) * 64 + lane];
+    }
+    ba1[Mt] = *(const f4*)(lds + BA1 + 16 * Mt + 4 * g);
+    bc1[Mt] = *(const f4*)(lds + BC1 + 16 * Mt + 4 * g);
+    ba2[Mt] = *(const f4*)(lds + BA2 + 16 * Mt + 4 * g);
+    wc2[Mt] = *(const f4*)(lds + WC2 + 16 * Mt + 4 * g);
+#pragma unroll
+    for (int d = 0; d < 4; d++) w3[d][Mt] = *(const f4*)(lds + W3 + d * 64 + 16 * Mt + 4 * g);
+  }
   const int nchunks = (ga.samples + 15) / 16;
   const int nw = gridDim.x * WAVES;
   // gather (CreateBatches, PPOAgent.cs:512-533), one chunk ahead of the math
@@ -131,43 +147,44 @@ void k_ppo_grad_mfma(GradArgs ga) {
     float sB[3];
 #pragma unroll
     for (int t = 0; t < 3; t++) sB[t] = cb[C_SX + n * 16 + 4 * t + g];
-    f4 z1[4], zc1[4], h1[4];
+    f4 z1[4], zc1[4], h1[4], hc1[4];
 #pragma unroll
     for (int Mt = 0; Mt < 4; Mt++) {
       f4 acc = z4, accc = z4;
 #pragma unroll
       for (int t = 0; t < 3; t++) {
-        acc = mfma(lds[AW1F + (Mt * 3 + t) * 64 + lane], sB[t], acc);
-        accc = mfma(lds[CW1F + (Mt * 3 + t) * 64 + lane], sB[t], accc);
+        acc = mfma(wa1[Mt][t], sB[t], acc);
+        accc = mfma(wc1[Mt][t], sB[t], accc);
       }
-      f4 hc;
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        const int j = 16 * Mt + 4 * g + r;
-        acc[r] = acc[r] + lds[BA1 + j];
-        accc[r] = accc[r] + lds[BC1 + j];
+        acc[r] = acc[r] + ba1[Mt][r];
+        accc[r] = accc[r] + bc1[Mt][r];
         h1[Mt][r] = mf_lrelu(acc[r]);
-        hc[r] = mf_lrelu(accc[r]);
+        hc1[Mt][r] = mf_lrelu(accc[r]);
       }
       z1[Mt] = acc;
       zc1[Mt] = accc;
       *(f4*)(cb + C_H1 + n * RS + 16 * Mt + 4 * g) = h1[Mt];
-      *(f4*)(cb + C_HC1 + n * RS + 16 * Mt + 4 * g) = hc;
+      *(f4*)(cb + C_HC1 + n * RS + 16 * Mt + 4 * g) = hc1[Mt];
     }
     // ---- layer 2 (B operand = layer 1's D registers) ----
+    f4 w2[4][4];
+#pragma unroll
+    for (int Mt = 0; Mt < 4; Mt++)
+#pragma unroll
+      for (int Mp = 0; Mp < 4; Mp++) w2[Mt][Mp] = *(const f4*)(lds + W2F + ((Mt * 4 + Mp) * 64 + lane) * 4);
     f4 z2[4], h2[4];
 #pragma unroll
     for (int Mt = 0; Mt < 4; Mt++) {
       f4 acc = z4;
 #pragma unroll
-      for (int Mp = 0; Mp < 4; Mp++) {
-        const f4 w = *(const f4*)(lds + W2F + ((Mt * 4 + Mp) * 64 + lane) * 4);
+      for (int Mp = 0; Mp < 4; Mp++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) acc = mfma(w[r], h1[Mp][r], acc);
-      }
+        for (int r = 0; r < 4; r++) acc = mfma(w2[Mt][Mp][r], h1[Mp][r], acc);
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        acc[r] = acc[r] + lds[BA2 + 16 * Mt + 4 * g + r];
+        acc[r] = acc[r] + ba2[Mt][r];
         h2[Mt][r] = mf_lrelu(acc[r]);
       }
       z2[Mt] = acc;
@@ -177,13 +194,11 @@ void k_ppo_grad_mfma(GradArgs ga) {
     float p3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, pv = 0.0f;
 #pragma unroll
     for (int Mt = 0; Mt < 4; Mt++) {
-      const f4 hc = *(const f4*)(cb + C_HC1 + n * RS + 16 * Mt + 4 * g);
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        const int k = 16 * Mt + 4 * g + r;
 #pragma unroll
-        for (int d = 0; d < 4; d++) p3[d] = p3[d] + lds[W3 + d * 64 + k] * h2[Mt][r];
-        pv = pv + lds[WC2 + k] * hc[r];
+        for (int d = 0; d < 4; d++) p3[d] = p3[d] + w3[d][Mt][r] * h2[Mt][r];
+        pv = pv + wc2[Mt][r] * hc1[Mt][r];
       }
     }
 #pragma unroll
@@ -222,7 +237,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
     float actorLoss = (prob * frac) * lcd;
     criticLoss = use ? criticLoss / ga.b_div : 0.0f;
     actorLoss = use ? actorLoss / ga.b_div : 0.0f;
-    const float th = tanhf(z3);
+    const float th = mean;  // tanh(z3) again in the reference's backward pass
     const float gz3 = actorLoss * (1.0f - (th * th));
     float al[4], q[4];
 #pragma unroll
@@ -239,76 +254,91 @@ void k_ppo_grad_mfma(GradArgs ga) {
     }
     db3 += gz3;
     cb[C_G3 + n * 16 + g] = gz3;
-    // ---- gh2 = W3^T gz3 -> gz2 ----
-    f4 gz2[4];
+    // ---- gh2 = W3^T gz3 -> gz2; critic gzc1 = (Wc2 dV) * lrelu'(zc1) ----
+    f4 gz2[4], gzc1[4];
 #pragma unroll
     for (int Mt = 0; Mt < 4; Mt++) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        const int k = 16 * Mt + 4 * g + r;
         float gh = 0.0f;
 #pragma unroll
-        for (int d = 0; d < 4; d++) gh = gh + lds[W3 + d * 64 + k] * q[d];
+        for (int d = 0; d < 4; d++) gh = gh + w3[d][Mt][r] * q[d];
         gz2[Mt][r] = gh * mf_dlrelu(z2[Mt][r]);
         db2[Mt * 4 + r] += gz2[Mt][r];
+        const float ghc1 = 0.0f + wc2[Mt][r] * criticLoss;  // same in the sample's 4 lanes
+        gzc1[Mt][r] = ghc1 * mf_dlrelu(zc1[Mt][r]);
       }
       *(f4*)(cb + C_G2 + n * RS + 16 * Mt + 4 * g) = gz2[Mt];
     }
     wave_sync();
     // ---- dW3 | dWc2 += [gz3; dV]^T [H2 | Hc1]; dW2 += gz2^T H1 (samples on K) ----
+    {
+      float av[4], bv[4][8], ag[4][4], bh[4][4];
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const int s = 4 * t + g;
-      const float av = cb[C_G3 + s * 16 + n];
+      for (int t = 0; t < 4; t++) {
+        const int s = 4 * t + g;
+        av[t] = cb[C_G3 + s * 16 + n];
 #pragma unroll
-      for (int Nt = 0; Nt < 4; Nt++) {
-        a3[Nt] = mfma(av, cb[C_H2 + s * RS + 16 * Nt + n], a3[Nt]);
-        a3[Nt + 4] = mfma(av, cb[C_HC1 + s * RS + 16 * Nt + n], a3[Nt + 4]);
+        for (int Nt = 0; Nt < 4; Nt++) {
+          bv[t][Nt] = cb[C_H2 + s * RS + 16 * Nt + n];
+          bv[t][Nt + 4] = cb[C_HC1 + s * RS + 16 * Nt + n];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          ag[t][i] = cb[C_G2 + s * RS + 16 * i + n];
+          bh[t][i] = cb[C_H1 + s * RS + 16 * i + n];
+        }
       }
-      float ag[4], bh[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        ag[i] = cb[C_G2 + s * RS + 16 * i + n];
-        bh[i] = cb[C_H1 + s * RS + 16 * i + n];
+      for (int t = 0; t < 4; t++) {
+#pragma unroll
+        for (int Nt = 0; Nt < 8; Nt++) a3[Nt] = mfma(av[t], bv[t][Nt], a3[Nt]);
+#pragma unroll
+        for (int Mj = 0; Mj < 4; Mj++)
+#pragma unroll
+          for (int Nk = 0; Nk < 4; Nk++) a2[Mj][Nk] = mfma(ag[t][Mj], bh[t][Nk], a2[Mj][Nk]);
       }
-#pragma unroll
-      for (int Mj = 0; Mj < 4; Mj++)
-#pragma unroll
-        for (int Nk = 0; Nk < 4; Nk++) a2[Mj][Nk] = mfma(ag[Mj], bh[Nk], a2[Mj][Nk]);
     }
     wave_sync();  // H2 / Hc1 reads done before G1 / Gc1 overwrite them
-    // ---- gh1^T = W2^T gz2^T (B = gz2 registers) -> gz1; critic gzc1 ----
+    // ---- gh1^T = W2^T gz2^T (B = gz2 registers) -> gz1 ----
+#pragma unroll
+    for (int Mk = 0; Mk < 4; Mk++)
+#pragma unroll
+      for (int Mj = 0; Mj < 4; Mj++) w2[Mk][Mj] = *(const f4*)(lds + W2B + ((Mk * 4 + Mj) * 64 + lane) * 4);
 #pragma unroll
     for (int Mk = 0; Mk < 4; Mk++) {
       f4 acc = z4;
 #pragma unroll
-      for (int Mj = 0; Mj < 4; Mj++) {
-        const f4 w = *(const f4*)(lds + W2B + ((Mk * 4 + Mj) * 64 + lane) * 4);
+      for (int Mj = 0; Mj < 4; Mj++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) acc = mfma(w[r], gz2[Mj][r], acc);
-      }
-      f4 gz1, gzc1;
+        for (int r = 0; r < 4; r++) acc = mfma(w2[Mk][Mj][r], gz2[Mj][r], acc);
+      f4 gz1;
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int k = 16 * Mk + 4 * g + r;
-        gz1[r] = acc[r] * mf_dlrelu(z1[Mk][r]);
-        const float ghc1 = 0.0f + lds[WC2 + k] * criticLoss;  // same in the sample's 4 lanes
-        gzc1[r] = ghc1 * mf_dlrelu(zc1[Mk][r]);
-      }
+      for (int r = 0; r < 4; r++) gz1[r] = acc[r] * mf_dlrelu(z1[Mk][r]);
       *(f4*)(cb + C_G1 + n * RS + 16 * Mk + 4 * g) = gz1;
-      *(f4*)(cb + C_GC1 + n * RS + 16 * Mk + 4 * g) = gzc1;
+      *(f4*)(cb + C_GC1 + n * RS + 16 * Mk + 4 * g) = gzc1[Mk];
     }
     wave_sync();
     // ---- dW1 | db1, dWc1 | dbc1 += gz1^T [S | 1] ----
+    {
+      float bx[4], a1v[4][4], a1cv[4][4];
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const int s = 4 * t + g;
-      const float bx = cb[C_SX + s * 16 + n];
+      for (int t = 0; t < 4; t++) {
+        const int s = 4 * t + g;
+        bx[t] = cb[C_SX + s * 16 + n];
 #pragma unroll
-      for (int Mj = 0; Mj < 4; Mj++) {
-        a1[Mj] = mfma(cb[C_G1 + s * RS + 16 * Mj + n], bx, a1[Mj]);
-        a1c[Mj] = mfma(cb[C_GC1 + s * RS + 16 * Mj + n], bx, a1c[Mj]);
+        for (int Mj = 0; Mj < 4; Mj++) {
+          a1v[t][Mj] = cb[C_G1 + s * RS + 16 * Mj + n];
+          a1cv[t][Mj] = cb[C_GC1 + s * RS + 16 * Mj + n];
+        }
       }
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int Mj = 0; Mj < 4; Mj++) {
+          a1[Mj] = mfma(a1v[t][Mj], bx[t], a1[Mj]);
+          a1c[Mj] = mfma(a1cv[t][Mj], bx[t], a1c[Mj]);
+        }
     }
     wave_sync();  // the next chunk rewrites every tile
   }

@@ -92,7 +92,8 @@ class Profile(C.Structure):
                 ("reduce_launches", C.c_int64), ("adam_ms", C.c_double),
                 ("adam_launches", C.c_int64), ("allreduce_ms", C.c_double),
                 ("allreduce_calls", C.c_int64), ("returns_ms", C.c_double),
-                ("returns_launches", C.c_int64)]
+                ("returns_launches", C.c_int64), ("update_ms", C.c_double),
+                ("update_calls", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -368,8 +369,13 @@ class Engine:
     def compute_returns(self):
         self._chk(self.lib.wk_compute_returns(self.h), "wk_compute_returns")
 
-    def ppo_update(self, epochs=0, minibatch=0, minibatch_global=0, update_index=0):
+    def ppo_update(self, epochs=0, minibatch=0, minibatch_global=0, update_index=0, sync=True):
+        """Whole PPO update; returns the last minibatch's (critic, actor) diagnostics, or
+        (None, None) with sync=False (then nothing waits on the stream)."""
         a = PpoArgs(int(epochs), int(minibatch), int(minibatch_global), int(update_index))
+        if not sync:
+            self._chk(self.lib.wk_ppo_update(self.h, C.byref(a), None, None), "wk_ppo_update")
+            return None, None
         cd, ad = C.c_float(), C.c_float()
         self._chk(self.lib.wk_ppo_update(self.h, C.byref(a), C.byref(cd), C.byref(ad)),
                   "wk_ppo_update")
@@ -419,7 +425,8 @@ class Engine:
 
     # -- profiling --
     def profile_enable(self, on=True):
-        self._chk(self.lib.wk_profile_enable(self.h, int(bool(on))), "wk_profile_enable")
+        """on: False/0 off, True/1 per rollout / update, 2 per kernel launch as well"""
+        self._chk(self.lib.wk_profile_enable(self.h, int(on)), "wk_profile_enable")
 
     def profile_reset(self):
         self._chk(self.lib.wk_profile_reset(self.h), "wk_profile_reset")
