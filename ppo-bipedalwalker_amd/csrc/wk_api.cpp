@@ -657,21 +657,10 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
     HIPCHK(c, wpb == 0 ? wk::launch_ppo_grad_mfma(g, nblocks, c->stream)
                        : wk::launch_ppo_grad(g, wpb, nblocks, c->stream));
   }
-  {
-    ProfScope ps(c, PK_REDUCE, 0, 2);
-    HIPCHK(c, wk::launch_grad_reduce(c->partial, nblocks, c->partial + (size_t)nblocks * wk::SLAB,
-                                     c->grad, c->stream));
-  }
-  if (c->comm && c->nranks > 1) {
-    ProfScope ps(c, PK_ALLRED, 0, 2);
-    ncclResult_t r = ncclAllReduce(c->grad, c->grad, wk::SLAB, ncclFloat, ncclSum,
-                                   c->comm, c->stream);
-    if (r != ncclSuccess) { SETERR(c, "ncclAllReduce: %s", ncclGetErrorString(r)); return WK_ERR_COMM; }
-  }
+  wk::AdamArgs a{};
   if (apply_adam) {
     c->adam_t += 1;
     const wk_config& k = c->cfg;
-    wk::AdamArgs a;
     a.W = c->W; a.m = c->m; a.v = c->v; a.grad = c->grad; a.Wz = c->Wz;
     a.c1 = 1.0f - k.Beta1;
     a.c2 = 1.0f - k.Beta2;
@@ -681,6 +670,25 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
     a.bc2 = (float)(1.0 - pow((double)k.Beta2, (double)c->adam_t));
     a.alpha = k.Alpha;
     a.eps = k.AdamEpsilon;
+  }
+  float* part2 = c->partial + (size_t)nblocks * wk::SLAB;
+  const bool multi = c->comm && c->nranks > 1;
+  if (apply_adam && !multi) {  // one GPU: the last reduction stage applies Adam
+    ProfScope ps(c, PK_REDUCE, 0, 2);
+    HIPCHK(c, wk::launch_grad_reduce_adam(c->partial, nblocks, part2, c->grad, a, c->stream));
+    return WK_OK;
+  }
+  {
+    ProfScope ps(c, PK_REDUCE, 0, 2);
+    HIPCHK(c, wk::launch_grad_reduce(c->partial, nblocks, part2, c->grad, c->stream));
+  }
+  if (multi) {
+    ProfScope ps(c, PK_ALLRED, 0, 2);
+    ncclResult_t r = ncclAllReduce(c->grad, c->grad, wk::SLAB, ncclFloat, ncclSum,
+                                   c->comm, c->stream);
+    if (r != ncclSuccess) { SETERR(c, "ncclAllReduce: %s", ncclGetErrorString(r)); return WK_ERR_COMM; }
+  }
+  if (apply_adam) {
     ProfScope ps(c, PK_ADAM, 0, 2);
     HIPCHK(c, wk::launch_adam(a, c->stream));
   }

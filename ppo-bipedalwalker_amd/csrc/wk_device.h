@@ -218,6 +218,38 @@ DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, 
   }
 }
 
+// SAT of A against the static floor (Environment.CreateFloor, Environment.cs:219-223).
+// The floor's four edge normals normalise to exactly (1,+0), (-0,1), (-1,+0), (-0,-1)
+// and its own projections onto them are constants; A's projections onto them
+// (1*x + 0*y, ...) equal A's bounding-box extents in value -- at most a zero's sign
+// differs, which never reaches depth on an overlapping axis -- so the floor's half of
+// AxisChecks needs no vertex loop.  Same verdict, normal and depth bits as sat().
+DEV void floor_axis(float pmin, float pmax, float qmin, float qmax, float nx, float ny, bool& sep,
+                    V2& normal, float& depth) {
+  const float temp = __builtin_fminf(qmax - pmin, pmax - qmin);
+  const bool overlapping = (pmin < qmax) && (qmin < pmax);
+  sep = sep || !overlapping;
+  const bool take = overlapping && temp < depth;
+  depth = take ? temp : depth;
+  normal.x = take ? nx : normal.x;
+  normal.y = take ? ny : normal.y;
+}
+template <int NA>
+DEV bool sat_floor(const Poly<NA>& A, const Poly<4>& F, float mnx, float mny, float mxx,
+                   float mxy, V2& normal, float& depth) {
+  normal = mk(0.0f, 0.0f);
+  depth = FLT_MAX;
+  bool sep = false;
+  axis_pass(A, F, sep, normal, depth);
+  floor_axis(-50.0f, 1050.0f, mnx, mxx, 1.0f, 0.0f, sep, normal, depth);
+  floor_axis(900.0f, 1050.0f, mny, mxy, -0.0f, 1.0f, sep, normal, depth);
+  floor_axis(-1050.0f, 50.0f, -mxx, -mnx, -1.0f, 0.0f, sep, normal, depth);
+  floor_axis(-1050.0f, -900.0f, -mxy, -mny, -0.0f, -1.0f, sep, normal, depth);
+  V2 dir = mk(F.cx - A.cx, F.cy - A.cy);
+  if (vdot(dir, normal) > 0.0f) normal = vmul(normal, -1.0f);
+  return !sep;
+}
+
 template <int NA, int NB>
 DEV bool sat(const Poly<NA>& A, const Poly<NB>& B, V2& normal, float& depth) {
   normal = mk(0.0f, 0.0f);

@@ -89,6 +89,8 @@ int ppo_grad_mfma_blocks(int samples);
 hipError_t launch_grad_reduce(const float* partial, int nblocks, float* part2, float* grad,
                               hipStream_t s);
 int grad_reduce_groups(int nblocks);
+hipError_t launch_grad_reduce_adam(const float* partial, int nblocks, float* part2, float* grad,
+                                   const AdamArgs& a, hipStream_t s);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t s);
 hipError_t launch_normalize(float* x, int n, float eps, hipStream_t s);
 hipError_t launch_xavier(float* W, uint64_t seed, hipStream_t s);

@@ -187,13 +187,43 @@ DEV void get_obs(const EnvState& s, float o[12]) {
   o[11] = s.drlu.th;
 }
 
+// Differential cost probes (build with -DWK_DUP=k, scripts/dup_probe.sh): region k runs a
+// second time on inputs perturbed by an opaque zero, results kept alive but unused.
+#ifdef WK_DUP
+DEV float opaque_zero() { float z; asm volatile("v_mov_b32 %0, 0" : "=v"(z)); return z; }
+DEV void sink(float v) { asm volatile("" ::"v"(v)); }
+template <int N>
+DEV Poly<N> perturbed(const Poly<N>& p) {
+  Poly<N> q = p;
+  const float z = opaque_zero();
+#pragma unroll
+  for (int i = 0; i < N; i++) { q.x[i] = q.x[i] + z; q.y[i] = q.y[i] + z; }
+  q.cx = q.cx + z; q.cy = q.cy + z;
+  return q;
+}
+#define DUP(k, ...) do { if (WK_DUP == (k)) { __VA_ARGS__ } } while (0)
+#else
+#define DUP(k, ...) do {} while (0)
+#endif
+
 // RigidBody.ResolveCollisions body for one (this=A, other=B) candidate
 // (Bodies/RigidBody.cs:66-96); B may be the static floor.
 template <int NA, int NB, bool BSTATIC, bool TRACE, int L>
 DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB,
                       bool& colA, PairTraceDev* tr, int pi, int sub, RegionProf* rp = nullptr) {
-  const bool ov = aabb_overlap(A, B);
+  static_assert(!BSTATIC || NB == 4, "the static body is the floor");
+  float mnx, mny, mxx, mxy;  // A's bounding box (the floor pass of sat_floor reuses it)
+  aabb(A, mnx, mny, mxx, mxy);
+  bool ov;
+  if constexpr (BSTATIC) {
+    ov = mnx < 1050.0f && mxx > -50.0f && mny < 1050.0f && mxy > 900.0f;  // floor box
+  } else {
+    float b0x, b0y, b1x, b1y;
+    aabb(B, b0x, b0y, b1x, b1y);
+    ov = mnx < b1x && mxx > b0x && mny < b1y && mxy > b0y;
+  }
   rp_mark(rp, RP_AABB);
+  DUP(1, { const auto Ap = perturbed(A); sink(aabb_overlap(Ap, B) ? 1.0f : 0.0f); });
   if (!ov) return;
   if (TRACE && tr) tr->aabb_hit[pi] = 1;
   if (BSTATIC) colA = true;  // body._isFloor -> Collided = true (:75)
@@ -201,12 +231,17 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   float depth;
   bool hit;
   if constexpr (L > 1) hit = sat_row<L>(A, B, sub, n, depth);
+  else if constexpr (BSTATIC) hit = sat_floor(A, B, mnx, mny, mxx, mxy, n, depth);
   else hit = sat(A, B, n, depth);
   rp_mark(rp, RP_SAT);
+  DUP(2, { const auto Ap = perturbed(A); V2 n2; float d2;
+           const bool h2 = sat(Ap, B, n2, d2); sink(n2.x); sink(n2.y); sink(d2); sink(h2 ? 1.0f : 0.0f); });
   if (!hit) return;
   V2 c0, c1;
   int nc = contact_points(A, B, n, c0, c1);
   rp_mark(rp, RP_CONTACT);
+  DUP(3, { const auto Ap = perturbed(A); V2 e0, e1;
+           const int k2 = contact_points(Ap, B, n, e0, e1); sink(e0.x); sink(e1.y); sink((float)k2); });
   if (TRACE && tr) {
     tr->sat_hit[pi] = 1;
     tr->n_contacts[pi] = (uint8_t)nc;
@@ -238,6 +273,14 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   apply_impulses<BSTATIC>(bA, bB, n, j, rA, rB);
   apply_impulses<BSTATIC>(bA, bB, tangent, jf, rAF, rBF);
   rp_mark(rp, RP_IMPULSE);
+  DUP(4, { Dyn dA2 = dA, dB2 = dB; const float z = opaque_zero();
+           Body cA{A.cx + z, A.cy, &dA2, mA.im, mA.ii}; Body cB{B.cx, B.cy, &dB2, mB.im, mB.ii};
+           V2 sA, sB, sAF, sBF;
+           const float j2 = calc_impulse(cA, cB, contact, 1.0f + e, n, sA, sB);
+           const float jf2 = calc_impulse(cA, cB, contact, mu, tangent, sAF, sBF);
+           apply_impulses<BSTATIC>(cA, cB, n, j2, sA, sB);
+           apply_impulses<BSTATIC>(cA, cB, tangent, jf2, sAF, sBF);
+           sink(dA2.vx); sink(dA2.w); sink(dB2.vy); });
 }
 
 // Joint.Step (Objects/RigidBodies/Joint.cs:31-41); ResolveJoint swaps the bodies (:40)
@@ -713,6 +756,9 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
   const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};
   // joints [bodyJointLeft, bodyJointRight, leftJoint, rightJoint] (Walker.cs:182-187)
   if (side == 0) joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.up, s.dup, mp, tr, 0);
+  DUP(5, { auto b2 = perturbed(s.body); auto u2 = s.up; Dyn db2 = s.dbody, du2 = s.dup;
+           joint_step<5, 6, 1, 4, false>(b2, db2, mb, u2, du2, mp, nullptr, 0);
+           sink(b2.cx); sink(u2.cy); sink(db2.w); sink(du2.vx); });
   bcast_torso<0xA0>(s.body, s.dbody);
   if (side == 1) joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.up, s.dup, mp, tr, 1);
   bcast_torso<0xF5>(s.body, s.dbody);
@@ -724,6 +770,8 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
   const int pb = side ? 5 : 0;
   integrate(s.lo, s.dlo, dt, adx, ady);
   rp_mark(rp, RP_INTEG);
+  DUP(6, { auto l2 = perturbed(s.lo); Dyn d2 = s.dlo; integrate(l2, d2, dt, adx, ady);
+           sink(l2.x[0]); sink(l2.y[5]); sink(d2.th); });
 #pragma unroll 1
   for (int q = 0; q < 3; q++) {  // [floor if post], other segment, [floor if episode 0]
     if (q == 1) resolve_pair<6, 6, false, TRACE, 1>(s.lo, s.dlo, mp, s.up, s.dup, mp, s.clo, tr, pb + 0, 0, rp);

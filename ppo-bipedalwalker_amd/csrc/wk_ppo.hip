@@ -279,11 +279,8 @@ __global__ void k_grad_reduce2(const float* __restrict__ part2, int ngroups, flo
   grad[p] = acc;
 }
 
-// DenseLayer.Adam (DenseLayer.cs:125-159), elementwise over all 6149 parameters
-__global__ void k_adam(AdamArgs a) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= NPARAM) return;
-  const float gr = a.grad[p];
+// DenseLayer.Adam (DenseLayer.cs:125-159) for one parameter
+DEV void adam_param(const AdamArgs& a, int p, float gr) {
   float m = (gr * a.c1) + (a.m[p] * a.beta1);
   float v = (a.v[p] * a.beta2) + ((gr * gr) * a.c2);
   a.m[p] = m;
@@ -294,6 +291,23 @@ __global__ void k_adam(AdamArgs a) {
   const float w = a.W[p] - ((mh / den) * a.alpha);
   a.W[p] = w;
   if (a.Wz) mf_scatter_param(a.Wz, p, w);
+}
+
+// elementwise over all 6149 parameters
+__global__ void k_adam(AdamArgs a) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < NPARAM) adam_param(a, p, a.grad[p]);
+}
+
+// single-GPU minibatch tail: the second reduction stage and Adam in one launch
+__global__ void k_grad_reduce2_adam(const float* __restrict__ part2, int ngroups, float* grad,
+                                    AdamArgs a) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= SLAB) return;
+  float acc = 0.0f;
+  for (int g = 0; g < ngroups; g++) acc = acc + part2[(size_t)g * SLAB + p];
+  grad[p] = acc;
+  if (p < NPARAM) adam_param(a, p, acc);
 }
 
 // Normalize (PPOAgent.cs:461-472): LINQ Average/Sum accumulate in double
@@ -381,6 +395,15 @@ hipError_t launch_grad_reduce(const float* partial, int nblocks, float* part2, f
   return hipGetLastError();
 }
 int grad_reduce_groups(int nblocks) { return (nblocks + RG - 1) / RG; }
+hipError_t launch_grad_reduce_adam(const float* partial, int nblocks, float* part2, float* grad,
+                                   const AdamArgs& a, hipStream_t s) {
+  const int ng = (nblocks + RG - 1) / RG;
+  hipLaunchKernelGGL(k_grad_reduce1, dim3((SLAB + 255) / 256, ng), dim3(256), 0, s, partial,
+                     nblocks, part2);
+  hipLaunchKernelGGL(k_grad_reduce2_adam, dim3((SLAB + 255) / 256), dim3(256), 0, s, part2, ng,
+                     grad, a);
+  return hipGetLastError();
+}
 hipError_t launch_adam(const AdamArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_adam, dim3((NPARAM + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();
