@@ -102,8 +102,10 @@ typedef struct wk_config {
   int EnvOffset;            /* global id of this context's env 0 (Philox streams) */
   int RandomizeStart;       /* 1: env e starts at x + 200*u_e (BASELINE config 2) */
   int RandomizeMaterial;    /* 1: env material in {Ice, Rubber, Carpet} (config 5) */
-  int LanesPerWalker;       /* physics kernel mapping: 0/16 = SAT axes over a 16-lane row,
-                               1 = one walker per lane (both bit-exact) */
+  int LanesPerWalker;       /* physics kernel mapping (all bit-exact): 2 = a lane pair per
+                               walker, left / right leg chains in parallel; 16 = SAT axes
+                               over a 16-lane row; 1 = one walker per lane; 0 = auto
+                               (2 from 32,768 walkers, else 16) */
 } wk_config;
 
 /* canonical per-env state dump: WK_STATE_FLOATS floats per env (identical layout to

@@ -13,13 +13,13 @@ fetch_csv, write_csv, walkers, horizon, out = sys.argv[1:6]
 
 def read(path, name):
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if r["Counter_Name"] == name and "k_env_step" in r["Kernel_Name"]]
+            if r["Counter_Name"] == name and "k_env_s" in r["Kernel_Name"]]
     return sum(vals) / len(vals), len(vals)
 
 
 f_kib, nf = read(fetch_csv, "FETCH_SIZE")
 w_kib, nw = read(write_csv, "WRITE_SIZE")
-res = {"kernel": "k_env_step<true,true,false>", "walkers": int(walkers), "horizon": int(horizon),
+res = {"kernel": "k_env_side<true,true,false> (rollout: physics + policy)", "walkers": int(walkers), "horizon": int(horizon),
        "fetch_size_kib": f_kib, "write_size_kib": w_kib,
        "hbm_bytes_per_launch": (2.0 * f_kib + w_kib) * 1024.0,
        "launches": [nf, nw],
