@@ -23,10 +23,11 @@ DEV V2 vneg(V2 a) { return mk(-a.x, -a.y); }
 DEV float vdot(V2 a, V2 b) { return a.x * b.x + a.y * b.y; }
 // Correctly rounded sqrt / reciprocal without the library's rescaling and special-value
 // fixups.  For x >= 2^-96 HIP's sqrtf is v_sqrt_f32 plus a one-ulp round-to-nearest
-// correction (below), and for a divisor in [2^-48, 2^64] its v_div_scale / v_div_fmas /
-// v_div_fixup sequence reduces to the Newton-Raphson FMAs of rcp_core: the same ops, so the
-// same bits (checked exhaustively over every float in range, tests/cpp/fastmath_check.hip).
-// Smaller inputs (never produced by walker-scale geometry) take the library path.
+// correction (sqrt_core: the same ops); for a divisor in [2^-48, 2^64] the reciprocal
+// needs only v_rcp_f32 and one Newton step (rcp_core).  Both are checked bit for bit
+// against sqrtf and 1.0f/x over every non-negative float (tests/cpp/fastmath_check.hip).
+// Inputs outside [2^-96, 2^126] (never produced by walker-scale geometry) take the
+// library path.
 DEV float sqrt_core(float x) {
   float s = __builtin_amdgcn_sqrtf(x);
   const float sd = __uint_as_float(__float_as_uint(s) - 1u);
@@ -36,15 +37,12 @@ DEV float sqrt_core(float x) {
   s = (ru > 0.0f) ? su : s;
   return s;
 }
+// v_rcp_f32 plus one Newton-Raphson step already equals the correctly rounded 1/d on
+// the whole domain (exhaustive: scripts/probe/fastmath_variants.hip, and the GPU test)
 DEV float rcp_core(float d) {
-  float r = __builtin_amdgcn_rcpf(d);
+  const float r = __builtin_amdgcn_rcpf(d);
   const float e = __builtin_fmaf(-d, r, 1.0f);
-  r = __builtin_fmaf(e, r, r);
-  float q = r;  // 1 * r
-  float rem = __builtin_fmaf(-d, q, 1.0f);
-  q = __builtin_fmaf(rem, r, q);
-  rem = __builtin_fmaf(-d, q, 1.0f);
-  return __builtin_fmaf(rem, r, q);
+  return __builtin_fmaf(e, r, r);
 }
 DEV bool fast_domain(float x) { return x >= 0x1p-96f && x <= 0x1p126f; }
 DEV float sqrt_rn(float x) {
