@@ -54,6 +54,14 @@ DEV float rsqrt_rn(float x) {
   if (__builtin_expect(!fast_domain(x), 0)) return 1.0f / sqrtf(x);
   return rcp_core(sqrt_core(x));
 }
+// Normalize for an edge of a walker polygon or the floor: rigid bodies keep their edge
+// lengths (7.5 .. 1100), so |e|^2 is inside the fast domain for every finite state and
+// the guard branch is dropped; a zero edge (masked by the caller) or a non-finite state
+// (already a fault) are the only inputs outside it.
+DEV V2 vnormalize_edge(V2 a) {
+  const float val = rcp_core(sqrt_core(a.x * a.x + a.y * a.y));
+  return mk(a.x * val, a.y * val);
+}
 DEV float vlen(V2 a) { return sqrt_rn(a.x * a.x + a.y * a.y); }
 DEV V2 vnormalize(V2 a) {
   float val = rsqrt_rn(a.x * a.x + a.y * a.y);
@@ -206,7 +214,7 @@ DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, 
     const float ex = P.x[i1] - P.x[i], ey = P.y[i1] - P.y[i];
     V2 axis = mk(-ey, ex);
     const bool valid = !(axis.x == 0.0f && axis.y == 0.0f);
-    axis = vnormalize(axis);  // NaN for a zero edge: masked by `valid`
+    axis = vnormalize_edge(axis);  // garbage for a zero edge: masked by `valid`
     float pmin, pmax, qmin, qmax;
     project2(axis.x, axis.y, P, Q, pmin, pmax, qmin, qmax);
     const float temp = __builtin_fminf(qmax - pmin, pmax - qmin);
@@ -396,8 +404,8 @@ DEV void significant_face(const Poly<N>& P, V2 n, V2& fa, V2& fb, V2& fmax) {
   const V2 sig = mk(__uint_as_float(sx), __uint_as_float(sy));
   const V2 va = mk(__uint_as_float(ax), __uint_as_float(ay));
   const V2 vb = mk(__uint_as_float(bx), __uint_as_float(by));
-  V2 after = vnormalize(vsub(sig, va));
-  V2 before = vnormalize(vsub(sig, vb));
+  V2 after = vnormalize_edge(vsub(sig, va));
+  V2 before = vnormalize_edge(vsub(sig, vb));
   const bool first = vdot(n, before) >= vdot(n, after);
   fa = first ? sig : va;
   fb = first ? vb : sig;
@@ -435,7 +443,7 @@ DEV int contact_points(const Poly<NA>& A, const Poly<NB>& B, V2 normal, V2& c0, 
     t = rmax; rmax = imax; imax = t;
     rf = vsub(rb, ra);
   }
-  rf = vnormalize(rf);
+  rf = vnormalize_edge(rf);  // rb - ra is an edge of the reference face
   float offset = vdot(rf, ra);
   V2 p0 = mk(0.0f, 0.0f), p1 = mk(0.0f, 0.0f);
   const int k1 = clip_vectors(ia, ib, rf, offset, p0, p1);
