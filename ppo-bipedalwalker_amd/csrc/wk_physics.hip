@@ -772,7 +772,7 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
   rp_mark(rp, RP_INTEG);
   DUP(6, { auto l2 = perturbed(s.lo); Dyn d2 = s.dlo; integrate(l2, d2, dt, adx, ady);
            sink(l2.x[0]); sink(l2.y[5]); sink(d2.th); });
-#pragma unroll 1
+#pragma unroll
   for (int q = 0; q < 3; q++) {  // [floor if post], other segment, [floor if episode 0]
     if (q == 1) resolve_pair<6, 6, false, TRACE, 1>(s.lo, s.dlo, mp, s.up, s.dup, mp, s.clo, tr, pb + 0, 0, rp);
     else if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1>(s.lo, s.dlo, mp, fl, dfl, mf, s.clo, tr, pb + 1, 0, rp);
@@ -780,7 +780,7 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
   }
   integrate(s.up, s.dup, dt, adx, ady);
   rp_mark(rp, RP_INTEG);
-#pragma unroll 1
+#pragma unroll
   for (int q = 0; q < 3; q++) {
     if (q == 1) resolve_pair<6, 6, false, TRACE, 1>(s.up, s.dup, mp, s.lo, s.dlo, mp, s.cup, tr, pb + 2, 0, rp);
     else if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1>(s.up, s.dup, mp, fl, dfl, mf, s.cup, tr, pb + 3, 0, rp);
