@@ -426,8 +426,9 @@ hipError_t launch_ppo_grad_mfma(const GradArgs& g, int nblocks, hipStream_t s) {
   const size_t lds = sizeof(float) * mf::LDS_FLOATS;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_ppo_grad_mfma,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipError_t e = hipFuncSetAttribute((const void*)k_ppo_grad_mfma,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
     attr_set = true;
   }
   hipLaunchKernelGGL(k_ppo_grad_mfma, dim3(nblocks), dim3(64 * mf::WAVES), lds, s, g);
