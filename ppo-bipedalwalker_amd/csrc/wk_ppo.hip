@@ -271,12 +271,27 @@ __global__ void k_grad_reduce1(const float* __restrict__ partial, int nblocks, f
   part2[(size_t)g * SLAB + p] = acc;
 }
 
+// stage 2: the groups in order; up to RG groups are loaded at once (one latency), more
+// fall back to a loop -- same association either way
+DEV float sum_groups(const float* __restrict__ part2, int ngroups, int p) {
+  if (ngroups <= RG) {
+    float v[RG];
+#pragma unroll
+    for (int g = 0; g < RG; g++) v[g] = g < ngroups ? part2[(size_t)g * SLAB + p] : 0.0f;
+    float acc = 0.0f;
+#pragma unroll
+    for (int g = 0; g < RG; g++)
+      if (g < ngroups) acc = acc + v[g];
+    return acc;
+  }
+  float acc = 0.0f;
+  for (int g = 0; g < ngroups; g++) acc = acc + part2[(size_t)g * SLAB + p];
+  return acc;
+}
 __global__ void k_grad_reduce2(const float* __restrict__ part2, int ngroups, float* grad) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= SLAB) return;
-  float acc = 0.0f;
-  for (int g = 0; g < ngroups; g++) acc = acc + part2[(size_t)g * SLAB + p];
-  grad[p] = acc;
+  grad[p] = sum_groups(part2, ngroups, p);
 }
 
 // DenseLayer.Adam (DenseLayer.cs:125-159) for one parameter
@@ -304,8 +319,7 @@ __global__ void k_grad_reduce2_adam(const float* __restrict__ part2, int ngroups
                                     AdamArgs a) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= SLAB) return;
-  float acc = 0.0f;
-  for (int g = 0; g < ngroups; g++) acc = acc + part2[(size_t)g * SLAB + p];
+  const float acc = sum_groups(part2, ngroups, p);
   grad[p] = acc;
   if (p < NPARAM) adam_param(a, p, acc);
 }
