@@ -811,6 +811,10 @@ DEV bool side_finite(const SideState& s) {
 // the four lane groups.  fp32 throughout; only the association of the k-sums differs
 // from the sequential reference (parity tests: rtol 1e-5).
 typedef float pf4 __attribute__((ext_vector_type(4)));
+DEV void st_nt4(float* p, float a, float b, float c, float d) {
+  const pf4 v = {a, b, c, d};
+  __builtin_nontemporal_store(v, (pf4*)p);
+}
 DEV pf4 pmfma(float a, float b, pf4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 DEV float plrelu(float z) { return z < 0.0f ? 0.2f * z : z; }  // == Math.Max(0.2 z, z), see mf_lrelu
 
@@ -959,16 +963,14 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArg
 #pragma unroll
       for (int d = 0; d < 4; d++) mean[d] = tanhf(z3[d]);
       sample_actions(P, A.lp_const, gid, t, mean, a, lp);
-      if (RECORD && leader) {
+      if (RECORD && leader) {  // streamed rows: 16-byte non-temporal stores keep the L2 for Wz
         const size_t idx = (size_t)(A.t0 + k) * n + e;
 #pragma unroll
-        for (int i = 0; i < 12; i++) A.traj_s[idx * 12 + i] = obs[i];
-#pragma unroll
-        for (int d = 0; d < 4; d++) {
-          A.traj_a[idx * 4 + d] = a[d];
-          A.traj_lp[idx * 4 + d] = lp[d];
-        }
-        A.traj_v[idx] = v;
+        for (int q = 0; q < 3; q++)
+          st_nt4(A.traj_s + idx * 12 + 4 * q, obs[4 * q], obs[4 * q + 1], obs[4 * q + 2], obs[4 * q + 3]);
+        st_nt4(A.traj_a + idx * 4, a[0], a[1], a[2], a[3]);
+        st_nt4(A.traj_lp + idx * 4, lp[0], lp[1], lp[2], lp[3]);
+        __builtin_nontemporal_store(v, A.traj_v + idx);
       }
     } else {
 #pragma unroll
@@ -1025,8 +1027,8 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArg
       if (A.done_out) A.done_out[(size_t)k * n + e] = terminal ? 1 : 0;
       if (RECORD) {
         const size_t idx = (size_t)(A.t0 + k) * n + e;
-        A.traj_r[idx] = reward;
-        A.traj_d[idx] = terminal ? 1 : 0;
+        __builtin_nontemporal_store(reward, A.traj_r + idx);
+        __builtin_nontemporal_store((uint8_t)(terminal ? 1 : 0), A.traj_d + idx);
       }
     }
     t++;
