@@ -922,8 +922,9 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], int side
   wave_lds_sync();  // outputs read before the next env-step rewrites the tile
 }
 
+constexpr int SIDE_BLOCK = 256;  // 4 waves: the policy's weight image is staged once per block
 template <bool POLICY, bool RECORD, bool TRACE>
-__global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArgs A) {
+__global__ __launch_bounds__(SIDE_BLOCK) WK_ENV_WPE void k_env_side(EnvParams P, StepArgs A) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int side = tid & 1;
   const int n = P.n_env;
@@ -932,7 +933,14 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArg
   const bool active = (tid >> 1) < n;
   const int e = active ? (tid >> 1) : n - 1;
   const bool leader = side == 0 && active;
-  __shared__ float pol_lds[POLICY ? 512 + 256 : 1];
+  __shared__ float pol_lds[POLICY ? (SIDE_BLOCK / 64) * 768 : 1];
+  __shared__ float wz_lds[POLICY ? mf::WEND : 1];  // operand-order weights (41 KB, 2 blocks/CU)
+  if (POLICY) {
+    for (int i = threadIdx.x; i < mf::WEND / 4; i += SIDE_BLOCK)
+      ((pf4*)wz_lds)[i] = ((const pf4*)A.Wz)[i];
+    __syncthreads();
+  }
+  float* const wave_pol = pol_lds + (POLICY ? (threadIdx.x >> 6) * 768 : 0);
   SideState s;
   load_side(s, A.st, e, side);
   const float dx = A.dxoff[e];
@@ -959,7 +967,7 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_side(EnvParams P, StepArg
     if (POLICY) {
       get_obs_side(s, side, obs);
       float z3[4], mean[4], v;
-      policy_mfma(A.Wz, obs, side, pol_lds, z3, v);
+      policy_mfma(wz_lds, obs, side, wave_pol, z3, v);
 #pragma unroll
       for (int d = 0; d < 4; d++) mean[d] = tanhf(z3[d]);
       sample_actions(P, A.lp_const, gid, t, mean, a, lp);
@@ -1139,7 +1147,7 @@ static void launch_lanes(int mode, const EnvParams& P, const StepArgs& A, hipStr
   }
 }
 static void launch_side(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
-  dim3 blk(64), grd((unsigned)(((size_t)P.n_env * 2 + 63) / 64));
+  dim3 blk(SIDE_BLOCK), grd((unsigned)(((size_t)P.n_env * 2 + SIDE_BLOCK - 1) / SIDE_BLOCK));
   switch (mode) {
     case 0: hipLaunchKernelGGL((k_env_side<false, false, false>), grd, blk, 0, s, P, A); break;
     case 1: hipLaunchKernelGGL((k_env_side<false, false, true>), grd, blk, 0, s, P, A); break;
