@@ -115,7 +115,11 @@ void k_ppo_grad_mfma(GradArgs ga) {
 #pragma unroll
     for (int d = 0; d < 4; d++) w3[d][Mt] = *(const f4*)(lds + W3 + d * 64 + 16 * Mt + 4 * g);
   }
+#ifdef WK_GRAD_NOLOOP  // probe: the launch without its chunk loop (fixed-cost measurement)
+  const int nchunks = 0;
+#else
   const int nchunks = (ga.samples + 15) / 16;
+#endif
   const int nw = gridDim.x * WAVES;
   // gather (CreateBatches, PPOAgent.cs:512-533), one chunk ahead of the math
   struct Smp { f4 sv; float act, lpo, ret, adv; };
@@ -354,9 +358,8 @@ void k_ppo_grad_mfma(GradArgs ga) {
 
   // ---- each wave writes its slab, then the block sums them in wave order ----
   __syncthreads();  // every wave is done with the weights and tiles
-  float* slab = lds + wave * SLAB;
-  for (int i = lane; i < SLAB; i += 64) slab[i] = 0.0f;
-  wave_sync();
+  float* slab = lds + wave * SLAB;  // every entry below is written exactly once
+  if (lane == 0) slab[NPARAM + 3] = 0.0f;  // (the pad)
 #pragma unroll
   for (int Mj = 0; Mj < 4; Mj++)
 #pragma unroll
