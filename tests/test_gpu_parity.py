@@ -369,3 +369,40 @@ def test_fast_sqrt_rcp_exhaustive():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 mismatches" in r.stdout
+
+
+def test_baseline_config2_physics_4096(wk, orc):
+    """BASELINE config 2: 4,096 walkers, physics-step only (auto mapping = 16-lane rows
+    below 32,768 walkers), 10 env-steps with given actions, bit-exact vs the oracle."""
+    n, k = 4096, 10
+    eng = wk.Engine(n, seed=SEED, RandomizeStart=1)
+    assert eng.cfg.LanesPerWalker == 0
+    rng = np.random.default_rng(42)
+    acts = rng.uniform(-1.1, 1.1, (k, n, 4)).astype(F)
+    obs, rew, done, fault = eng.step(acts, k=k)
+    envs = [orc.Env(dx=float(orc.env_offset(SEED, e))) for e in range(n)]
+    for i, e in enumerate(envs):
+        for t in range(k):
+            e.step(acts[t, i])
+    np.testing.assert_array_equal(eng.get_state(), np.stack([e.dump() for e in envs]))
+    assert not fault.any()
+
+
+def test_baseline_config3_rollout_update_4096(wk, orc):
+    """BASELINE config 3: 4,096 walkers, full rollout + PPO update on one GPU: the
+    recorded actions replay bit-exactly through the oracle's physics, and the update
+    leaves finite weights that moved."""
+    n, T = 4096, 8
+    eng = wk.Engine(n, seed=SEED, Horizon=T, RandomizeStart=1, Minibatch=4096, Epochs=2)
+    w0 = eng.get_weights()
+    eng.rollout(T)
+    tr = eng.get_trajectory(T)
+    envs = [orc.Env(dx=float(orc.env_offset(SEED, e))) for e in range(n)]
+    for i, e in enumerate(envs):
+        for t in range(T):
+            o, r, d = e.step(tr["actions"][t, i])
+            assert r == tr["rewards"][t, i] and d == tr["dones"][t, i]
+    np.testing.assert_array_equal(eng.get_state(), np.stack([e.dump() for e in envs]))
+    eng.ppo_update(update_index=0)
+    w1 = eng.get_weights()
+    assert np.isfinite(w1).all() and not np.array_equal(w0, w1)
