@@ -347,6 +347,9 @@ void k_ppo_grad_mfma(GradArgs ga) {
     wave_sync();  // the next chunk rewrites every tile
   }
 
+#ifdef WK_GRAD_NOEPI  // probe: no epilogue
+  if (ga.samples >= 0) return;
+#endif
   // ---- per-lane sums over the 16 sample lanes of each row ----
 #pragma unroll
   for (int i = 0; i < 16; i++) db2[i] = row_sum16(db2[i]);
