@@ -202,6 +202,28 @@ int wk_get_weights(wk_ctx* ctx, float* params /* WK_NPARAM */);
 int wk_set_weights(wk_ctx* ctx, const float* params);
 int wk_get_adam(wk_ctx* ctx, float* m, float* v, int* t);
 int wk_set_adam(wk_ctx* ctx, const float* m, const float* v, int t);
+
+/* Weights files in the reference's text format (replaces PPOAgent.Save / Load,
+ * PPOAgent.cs:192-213, over NeuralNetwork.Save / Load NeuralNetwork.cs:94-176,
+ * DenseLayer.Save / Load DenseLayer.cs:55-79, Matrix.Save / Load Matrix.cs:109-153):
+ * line 0 the network DSL string, then per dense layer "W <out*in row-major> B <out>",
+ * floats written as .NET Core's float.ToString() (shortest round-trip, "1E-05" style).
+ * Unlike the reference (which silently keeps its weights), a mismatching DSL line or a
+ * malformed token is an error (WK_ERR_CONFIG / WK_ERR_ARG) and nothing is changed. */
+int wk_save_weights(wk_ctx* ctx, const char* critic_path, const char* actor_path);
+int wk_load_weights(wk_ctx* ctx, const char* critic_path, const char* actor_path);
+/* context-free text conversion of a WK_NPARAM vector (no GPU).  wk_format_weights returns
+ * -(bytes needed) when a buffer is too small. */
+int wk_format_weights(const float* params, char* critic_text, size_t critic_cap,
+                      char* actor_text, size_t actor_cap);
+int wk_parse_weights(const char* critic_text, const char* actor_text, float* params);
+
+/* Binary checkpoint for bit-exact resume (new; the reference persists only weights):
+ * weights, Adam m / v / t, every walker record, Philox step counters, start offsets and
+ * materials.  Loading requires the same n_env, seed and EnvOffset; it invalidates the
+ * trajectory buffer (roll out again before wk_ppo_update). */
+int wk_checkpoint_save(wk_ctx* ctx, const char* path);
+int wk_checkpoint_load(wk_ctx* ctx, const char* path);
 int wk_policy_sample(wk_ctx* ctx, int n, const float* obs /* n*12 */, const int32_t* env_ids,
                      const uint32_t* steps, float* mean, float* act, float* logp);
 int wk_value(wk_ctx* ctx, int n, const float* obs, float* v);

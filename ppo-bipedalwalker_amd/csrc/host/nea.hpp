@@ -28,6 +28,8 @@
 #include <tuple>
 #include <vector>
 
+#include <sys/stat.h>
+
 #include "../../../include/wk_api.h"
 
 namespace NEA {
@@ -139,6 +141,26 @@ class PPOAgent {
   void Load(const std::vector<float>& p) {
     if (p.size() != (size_t)WK_NPARAM) { LogError("Loading weights with the wrong size."); return; }
     if (wk_set_weights(ctx_, p.data()) != WK_OK) LogError(wk_last_error(ctx_));
+  }
+  // PPOAgent.Save (PPOAgent.cs:192-213): <filePath>Data/Weights/<critic|actor>.weights in
+  // the reference's text format; the directory is created like Hyperparameters.CreateDirectories
+  void Save(const std::string& filePath, const std::string& criticName = "critic",
+            const std::string& actorName = "actor") {
+    const std::string dir = filePath + "Data/Weights/";
+    ::mkdir((filePath + "Data").c_str(), 0755);
+    ::mkdir(dir.c_str(), 0755);
+    if (wk_save_weights(ctx_, (dir + criticName + ".weights").c_str(),
+                        (dir + actorName + ".weights").c_str()) != WK_OK)
+      LogError(std::string("Exception while attempting to save the critic and actor neural networks: ") +
+               wk_last_error(ctx_));
+  }
+  // NeuralNetwork.Load (NeuralNetwork.cs:94-115) for both networks from the same files
+  void Load(const std::string& filePath, const std::string& criticName = "critic",
+            const std::string& actorName = "actor") {
+    const std::string dir = filePath + "Data/Weights/";
+    if (wk_load_weights(ctx_, (dir + criticName + ".weights").c_str(),
+                        (dir + actorName + ".weights").c_str()) != WK_OK)
+      LogError(std::string("Loading neural network weights: ") + wk_last_error(ctx_));
   }
  private:
   wk_ctx* ctx_;

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -869,6 +870,264 @@ int wk_profile_get(wk_ctx* c, wk_profile* o) {
   o->allreduce_ms = c->prof_ms[PK_ALLRED]; o->allreduce_calls = c->prof_cnt[PK_ALLRED];
   o->returns_ms = c->prof_ms[PK_RET]; o->returns_launches = c->prof_cnt[PK_RET];
   o->update_ms = c->prof_ms[PK_UPDATE]; o->update_calls = c->prof_cnt[PK_UPDATE];
+  return WK_OK;
+}
+
+}  // extern "C"
+
+// ---------------- weights text format + binary checkpoint ----------
+// Reference format (PPOAgent.Save PPOAgent.cs:192-213 -> NeuralNetwork.Save
+// NeuralNetwork.cs:159-176 -> DenseLayer.Save DenseLayer.cs:73-79 -> Matrix.Save
+// Matrix.cs:133-153): one file per network, line 0 the network DSL string, then one line
+// per dense layer "W w00 w01 ... B b0 b1 ..." (row-major out x in, values joined by one
+// space).  Values are written as .NET Core 3.0+'s float.ToString() writes them under
+// en-US: shortest round-trip digits, "E-05" / "E+09"-style exponents for |v| < 1e-4 or
+// >= 1e9, "-0", "NaN", "∞".  Parsing accepts strtof syntax plus "∞" (a superset of the
+// digit strings float.Parse reads; "Infinity" and "NaN" included).
+
+namespace {
+struct DenseSpec { int off_w, rows, cols, off_b; };
+const DenseSpec kCriticLayers[] = {{wk::OFF_C_W1, 64, 12, wk::OFF_C_B1}, {wk::OFF_C_W2, 1, 64, wk::OFF_C_B2}};
+const DenseSpec kActorLayers[] = {{wk::OFF_A_W1, 64, 12, wk::OFF_A_B1},
+                                  {wk::OFF_A_W2, 64, 64, wk::OFF_A_B2},
+                                  {wk::OFF_A_W3, 4, 64, wk::OFF_A_B3}};
+
+std::string dotnet_float(float v) {
+  if (std::isnan(v)) return "NaN";
+  if (std::isinf(v)) return v > 0 ? "\xe2\x88\x9e" : "-\xe2\x88\x9e";  // .NET Core 3.0+: "∞"
+  if (v == 0.0f) return std::signbit(v) ? "-0" : "0";
+  char buf[64];
+  int prec = 1;
+  for (; prec <= 9; prec++) {  // shortest round-trip significant digits
+    snprintf(buf, sizeof buf, "%.*e", prec - 1, (double)v);
+    if (strtof(buf, nullptr) == v) break;
+  }
+  // buf = "[-]d.ddde[+-]XX": split mantissa digits and exponent
+  std::string s(buf);
+  const size_t epos = s.find('e');
+  const int exp10 = atoi(s.c_str() + epos + 1);
+  std::string mant = s.substr(0, epos);
+  const bool neg = mant[0] == '-';
+  if (neg) mant = mant.substr(1);
+  std::string digits;
+  for (char ch : mant)
+    if (ch != '.') digits += ch;
+  while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+  std::string out = neg ? "-" : "";
+  // Number.Formatting FormatGeneral: scientific when the decimal-point position
+  // (exp10 + 1) exceeds max(digit count, SinglePrecision = 9) or is below -3
+  const int scale = exp10 + 1;
+  if (scale > std::max((int)digits.size(), 9) || scale < -3) {  // d[.ddd]E+XX
+    out += digits[0];
+    if (digits.size() > 1) out += "." + digits.substr(1);
+    char eb[16];
+    snprintf(eb, sizeof eb, "E%c%02d", exp10 < 0 ? '-' : '+', exp10 < 0 ? -exp10 : exp10);
+    out += eb;
+  } else if (exp10 < 0) {
+    out += "0." + std::string(-exp10 - 1, '0') + digits;
+  } else {
+    if ((int)digits.size() <= exp10 + 1) {
+      out += digits + std::string(exp10 + 1 - digits.size(), '0');
+    } else {
+      out += digits.substr(0, exp10 + 1) + "." + digits.substr(exp10 + 1);
+    }
+  }
+  return out;
+}
+
+std::string format_network(const float* p, const char* dsl, const DenseSpec* layers, int nl) {
+  std::string text = std::string(dsl) + "\n";
+  for (int l = 0; l < nl; l++) {
+    const DenseSpec& d = layers[l];
+    std::string line = "W";
+    for (int i = 0; i < d.rows * d.cols; i++) line += " " + dotnet_float(p[d.off_w + i]);
+    line += " B";
+    for (int i = 0; i < d.rows; i++) line += " " + dotnet_float(p[d.off_b + i]);
+    text += line + "\n";
+  }
+  return text;
+}
+
+// NeuralNetwork.Load / ValidateWeights / DenseLayer.Load semantics: the DSL line must
+// match, every token must parse, and each layer needs rows*cols weights then rows biases.
+int parse_network(const char* text, const char* dsl, const DenseSpec* layers, int nl, float* p,
+                  std::string& why) {
+  std::vector<std::string> lines;
+  std::string cur;
+  for (const char* q = text; *q; q++) {
+    if (*q == '\n') { lines.push_back(cur); cur.clear(); }
+    else if (*q != '\r') cur += *q;
+  }
+  if (!cur.empty()) lines.push_back(cur);
+  if ((int)lines.size() < nl + 1) { why = "weights file too short"; return WK_ERR_ARG; }
+  if (lines[0] != dsl) { why = "network string '" + lines[0] + "' does not match '" + dsl + "'"; return WK_ERR_CONFIG; }
+  for (int l = 0; l < nl; l++) {
+    const DenseSpec& d = layers[l];
+    const std::string& s = lines[l + 1];
+    const size_t w = s.find('W'), b = s.find('B');
+    if (w == std::string::npos || b == std::string::npos || b < w) { why = "weights structure issue"; return WK_ERR_ARG; }
+    // "W a b c B d e": tokens separated by single spaces (ValidateWeights splits with
+    // string.Split(), so an empty token fails float.TryParse)
+    auto parse_list = [&](const std::string& seg, float* dst, int count) -> bool {
+      if (seg.size() < 2 || seg.front() != ' ') return false;
+      size_t at = 1;
+      for (int i = 0; i < count; i++) {
+        const size_t sp = seg.find(' ', at);
+        const std::string tok = seg.substr(at, sp == std::string::npos ? std::string::npos : sp - at);
+        if (tok.empty()) return false;
+        if (tok == "\xe2\x88\x9e") dst[i] = INFINITY;
+        else if (tok == "-\xe2\x88\x9e") dst[i] = -INFINITY;
+        else {
+          char* end = nullptr;
+          dst[i] = strtof(tok.c_str(), &end);
+          if (*end) return false;
+        }
+        if (sp == std::string::npos) return i == count - 1;
+        at = sp + 1;
+      }
+      return at == seg.size();  // the weights segment ends with the space before "B"
+    };
+    if (!parse_list(s.substr(w + 1, b - w - 1), p + d.off_w, d.rows * d.cols)) { why = "error in weights section"; return WK_ERR_ARG; }
+    if (!parse_list(s.substr(b + 1), p + d.off_b, d.rows)) { why = "error in biases section"; return WK_ERR_ARG; }
+  }
+  return WK_OK;
+}
+
+bool read_file(const char* path, std::string& out) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return false;
+  char buf[65536];
+  size_t k;
+  while ((k = fread(buf, 1, sizeof buf, f)) > 0) out.append(buf, k);
+  fclose(f);
+  return true;
+}
+bool write_file(const char* path, const void* data, size_t n) {
+  FILE* f = fopen(path, "wb");
+  if (!f) return false;
+  const bool ok = fwrite(data, 1, n, f) == n;
+  return fclose(f) == 0 && ok;
+}
+
+const uint32_t kCkptMagic = 0x4B434B57u;  // "WKCK"
+struct CkptHeader {
+  uint32_t magic, version, n_env, nstate, nparam, adam_t;
+  uint64_t seed;
+  int32_t env_offset, iterations, max_timesteps, pad;
+};
+}  // namespace
+
+extern "C" {
+
+int wk_format_weights(const float* params, char* critic, size_t critic_cap, char* actor,
+                      size_t actor_cap) {
+  if (!params) return WK_ERR_ARG;
+  const std::string c = format_network(params, kCriticDefault, kCriticLayers, 2);
+  const std::string a = format_network(params, kActorDefault, kActorLayers, 3);
+  if (!critic || !actor || critic_cap < c.size() + 1 || actor_cap < a.size() + 1)
+    return -(int)(c.size() > a.size() ? c.size() + 1 : a.size() + 1);  // needed capacity
+  memcpy(critic, c.c_str(), c.size() + 1);
+  memcpy(actor, a.c_str(), a.size() + 1);
+  return WK_OK;
+}
+
+int wk_parse_weights(const char* critic, const char* actor, float* params) {
+  if (!critic || !actor || !params) { g_create_error = "null argument"; return WK_ERR_ARG; }
+  std::vector<float> p(wk::NPARAM, 0.0f);
+  std::string why;
+  int r = parse_network(critic, kCriticDefault, kCriticLayers, 2, p.data(), why);
+  if (r == WK_OK) r = parse_network(actor, kActorDefault, kActorLayers, 3, p.data(), why);
+  if (r != WK_OK) { g_create_error = why; return r; }
+  memcpy(params, p.data(), sizeof(float) * wk::NPARAM);
+  return WK_OK;
+}
+
+int wk_save_weights(wk_ctx* c, const char* critic_path, const char* actor_path) {
+  if (!c || !critic_path || !actor_path) return WK_ERR_ARG;
+  std::vector<float> p(wk::NPARAM);
+  int r = wk_get_weights(c, p.data());
+  if (r) return r;
+  const std::string ct = format_network(p.data(), kCriticDefault, kCriticLayers, 2);
+  const std::string at = format_network(p.data(), kActorDefault, kActorLayers, 3);
+  if (!write_file(critic_path, ct.data(), ct.size()) || !write_file(actor_path, at.data(), at.size())) {
+    SETERR(c, "cannot write weights files '%s' / '%s'", critic_path, actor_path);
+    return WK_ERR_ARG;
+  }
+  return WK_OK;
+}
+
+int wk_load_weights(wk_ctx* c, const char* critic_path, const char* actor_path) {
+  if (!c || !critic_path || !actor_path) return WK_ERR_ARG;
+  std::string ct, at;
+  if (!read_file(critic_path, ct) || !read_file(actor_path, at)) {
+    SETERR(c, "cannot read weights files '%s' / '%s'", critic_path, actor_path);
+    return WK_ERR_ARG;
+  }
+  std::vector<float> p(wk::NPARAM, 0.0f);
+  std::string why;
+  int r = parse_network(ct.c_str(), kCriticDefault, kCriticLayers, 2, p.data(), why);
+  if (r == WK_OK) r = parse_network(at.c_str(), kActorDefault, kActorLayers, 3, p.data(), why);
+  if (r != WK_OK) { c->err = why; return r; }
+  return wk_set_weights(c, p.data());
+}
+
+// Binary checkpoint for exact resume: weights, Adam m / v / t, every walker record,
+// Philox step counters, start offsets and materials.
+int wk_checkpoint_save(wk_ctx* c, const char* path) {
+  if (!c || !path) return WK_ERR_ARG;
+  const size_t n = c->n;
+  CkptHeader h{kCkptMagic, 1u, (uint32_t)n, (uint32_t)wk::NSTATE, (uint32_t)wk::NPARAM,
+               (uint32_t)c->adam_t, c->seed, c->cfg.EnvOffset, c->cfg.Iterations,
+               c->cfg.MaxTimesteps, 0};
+  std::vector<char> buf(sizeof h + sizeof(float) * (3 * wk::NPARAM + n * wk::NSTATE + 2 * n) +
+                        sizeof(int32_t) * n);
+  char* q = buf.data();
+  memcpy(q, &h, sizeof h); q += sizeof h;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(q, c->W, sizeof(float) * wk::NPARAM, hipMemcpyDeviceToHost)); q += sizeof(float) * wk::NPARAM;
+  HIPCHK(c, hipMemcpy(q, c->m, sizeof(float) * wk::NPARAM, hipMemcpyDeviceToHost)); q += sizeof(float) * wk::NPARAM;
+  HIPCHK(c, hipMemcpy(q, c->v, sizeof(float) * wk::NPARAM, hipMemcpyDeviceToHost)); q += sizeof(float) * wk::NPARAM;
+  HIPCHK(c, hipMemcpy(q, c->st, sizeof(float) * n * wk::NSTATE, hipMemcpyDeviceToHost)); q += sizeof(float) * n * wk::NSTATE;
+  HIPCHK(c, hipMemcpy(q, c->rng_t, sizeof(uint32_t) * n, hipMemcpyDeviceToHost)); q += sizeof(uint32_t) * n;
+  HIPCHK(c, hipMemcpy(q, c->dxoff, sizeof(float) * n, hipMemcpyDeviceToHost)); q += sizeof(float) * n;
+  HIPCHK(c, hipMemcpy(q, c->mat, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  if (!write_file(path, buf.data(), buf.size())) { SETERR(c, "cannot write checkpoint '%s'", path); return WK_ERR_ARG; }
+  return WK_OK;
+}
+
+int wk_checkpoint_load(wk_ctx* c, const char* path) {
+  if (!c || !path) return WK_ERR_ARG;
+  std::string data;
+  if (!read_file(path, data)) { SETERR(c, "cannot read checkpoint '%s'", path); return WK_ERR_ARG; }
+  const size_t n = c->n;
+  CkptHeader h;
+  if (data.size() < sizeof h) { SETERR(c, "checkpoint '%s' truncated", path); return WK_ERR_ARG; }
+  memcpy(&h, data.data(), sizeof h);
+  const size_t need = sizeof h + sizeof(float) * (3 * wk::NPARAM + n * wk::NSTATE + 2 * n) + sizeof(int32_t) * n;
+  if (h.magic != kCkptMagic || h.version != 1u) { SETERR(c, "'%s' is not a wk checkpoint", path); return WK_ERR_ARG; }
+  if (h.n_env != n || h.nstate != (uint32_t)wk::NSTATE || h.nparam != (uint32_t)wk::NPARAM || data.size() != need) {
+    SETERR(c, "checkpoint '%s' is for %u walkers (context has %zu)", path, h.n_env, n);
+    return WK_ERR_ARG;
+  }
+  if (h.seed != c->seed || h.env_offset != c->cfg.EnvOffset) {  // the Philox streams differ
+    SETERR(c, "checkpoint '%s' was written with seed %llu / EnvOffset %d (context: %llu / %d)",
+           path, (unsigned long long)h.seed, h.env_offset, (unsigned long long)c->seed, c->cfg.EnvOffset);
+    return WK_ERR_CONFIG;
+  }
+  const char* q = data.data() + sizeof h;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(c->W, q, sizeof(float) * wk::NPARAM, hipMemcpyHostToDevice)); q += sizeof(float) * wk::NPARAM;
+  HIPCHK(c, hipMemcpy(c->m, q, sizeof(float) * wk::NPARAM, hipMemcpyHostToDevice)); q += sizeof(float) * wk::NPARAM;
+  HIPCHK(c, hipMemcpy(c->v, q, sizeof(float) * wk::NPARAM, hipMemcpyHostToDevice)); q += sizeof(float) * wk::NPARAM;
+  HIPCHK(c, hipMemcpy(c->st, q, sizeof(float) * n * wk::NSTATE, hipMemcpyHostToDevice)); q += sizeof(float) * n * wk::NSTATE;
+  HIPCHK(c, hipMemcpy(c->rng_t, q, sizeof(uint32_t) * n, hipMemcpyHostToDevice)); q += sizeof(uint32_t) * n;
+  HIPCHK(c, hipMemcpy(c->dxoff, q, sizeof(float) * n, hipMemcpyHostToDevice)); q += sizeof(float) * n;
+  HIPCHK(c, hipMemcpy(c->mat, q, sizeof(int32_t) * n, hipMemcpyHostToDevice));
+  c->adam_t = (int)h.adam_t;
+  c->T_valid = 0;
+  c->returns_valid = 0;
+  HIPCHK(c, wk::launch_swizzle(c->W, c->Wz, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return WK_OK;
 }
 

@@ -30,7 +30,8 @@ EXPORTS = [
     "wk_get_body_view", "wk_get_weights", "wk_set_weights", "wk_get_adam", "wk_set_adam",
     "wk_policy_sample", "wk_value", "wk_rollout", "wk_rollout_stats_get", "wk_get_trajectory",
     "wk_set_trajectory", "wk_compute_returns", "wk_ppo_update", "wk_train_batch",
-    "wk_minibatch_gradient",
+    "wk_minibatch_gradient", "wk_save_weights", "wk_load_weights", "wk_format_weights",
+    "wk_parse_weights", "wk_checkpoint_save", "wk_checkpoint_load",
     "wk_comm_unique_id", "wk_comm_init", "wk_allreduce_test", "wk_profile_enable",
     "wk_profile_get", "wk_profile_reset",
 ]
@@ -154,6 +155,12 @@ def load_library(path=None):
         "wk_ppo_update": (I, [P, C.POINTER(PpoArgs), fp, fp]),
         "wk_train_batch": (I, [P, I, F, P, P, P, P, P, fp, fp, P, I, C.POINTER(C.c_int)]),
         "wk_minibatch_gradient": (I, [P, I, F, P, P, P, P, P, fp, fp, P, C.POINTER(C.c_int)]),
+        "wk_save_weights": (I, [P, C.c_char_p, C.c_char_p]),
+        "wk_load_weights": (I, [P, C.c_char_p, C.c_char_p]),
+        "wk_format_weights": (I, [P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]),
+        "wk_parse_weights": (I, [C.c_char_p, C.c_char_p, P]),
+        "wk_checkpoint_save": (I, [P, C.c_char_p]),
+        "wk_checkpoint_load": (I, [P, C.c_char_p]),
         "wk_comm_unique_id": (I, [P]),
         "wk_comm_init": (I, [P, I, I, P]),
         "wk_allreduce_test": (I, [P, P, I]),
@@ -197,6 +204,31 @@ def default_config(**overrides):
             v = v.encode()
         setattr(c, k, v)
     return c
+
+
+def format_weights(params):
+    """(critic_text, actor_text) of a WK_NPARAM vector in the reference's weights-file format
+    (NeuralNetwork.Save NeuralNetwork.cs:159-176; one line per entry, newline-terminated)."""
+    lib = load_library()
+    p = _f32(params, (NPARAM,))
+    need = -lib.wk_format_weights(_ptr(p), None, 0, None, 0)
+    if need <= 0:
+        raise WkError("wk_format_weights: size query failed")
+    cb, ab = C.create_string_buffer(need), C.create_string_buffer(need)
+    rc = lib.wk_format_weights(_ptr(p), cb, need, ab, need)
+    if rc != 0:
+        raise WkError(f"wk_format_weights failed ({rc})")
+    return cb.value.decode(), ab.value.decode()
+
+
+def parse_weights(critic_text, actor_text):
+    """WK_NPARAM vector from weights-file texts (NeuralNetwork.Load NeuralNetwork.cs:94-115)."""
+    lib = load_library()
+    p = np.empty(NPARAM, np.float32)
+    rc = lib.wk_parse_weights(critic_text.encode(), actor_text.encode(), _ptr(p))
+    if rc != 0:
+        raise WkError(f"wk_parse_weights failed ({rc}): {lib.wk_last_error(None).decode()}")
+    return p
 
 
 class Engine:
@@ -314,6 +346,23 @@ class Engine:
         m = _f32(m, (NPARAM,))
         v = _f32(v, (NPARAM,))
         self._chk(self.lib.wk_set_adam(self.h, _ptr(m), _ptr(v), int(t)), "wk_set_adam")
+
+    def save_weights(self, critic_path, actor_path):
+        """PPOAgent.Save (PPOAgent.cs:192-213): critic / actor weights text files."""
+        self._chk(self.lib.wk_save_weights(self.h, os.fsencode(critic_path), os.fsencode(actor_path)),
+                  "wk_save_weights")
+
+    def load_weights(self, critic_path, actor_path):
+        """PPOAgent.Load over NeuralNetwork.Load (NeuralNetwork.cs:94-115), strict errors."""
+        self._chk(self.lib.wk_load_weights(self.h, os.fsencode(critic_path), os.fsencode(actor_path)),
+                  "wk_load_weights")
+
+    def checkpoint_save(self, path):
+        """Binary checkpoint: weights, Adam state, walker records and Philox counters."""
+        self._chk(self.lib.wk_checkpoint_save(self.h, os.fsencode(path)), "wk_checkpoint_save")
+
+    def checkpoint_load(self, path):
+        self._chk(self.lib.wk_checkpoint_load(self.h, os.fsencode(path)), "wk_checkpoint_load")
 
     def policy_sample(self, obs, env_ids=None, steps=None):
         obs = _f32(obs)

@@ -1,7 +1,7 @@
 // Drives the C++ host mirror (csrc/host/nea.hpp) the way the reference's Game1.Update
 // drives Environment.Update, and prints per-step rewards/dones and the final state so
 // tests/test_gpu_parity.py can compare them with the oracle.
-//   test_nea <n_walkers> <steps> <mode: actions|policy>
+//   test_nea <n_walkers> <steps> <mode: actions|policy> [weights dir: PPOAgent.Save there]
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -36,5 +36,6 @@ int main(int argc, char** argv) {
   }
   auto pos = env.GetWalker(0).GetPosition();
   printf("P %.9g %.9g\n", pos.first, pos.second);
+  if (argc > 4) env.Brain().Save(argv[4]);
   return 0;
 }

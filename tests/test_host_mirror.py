@@ -48,3 +48,17 @@ def test_mirror_matches_oracle(tmp_path, wk, orc):
     states = {int(l.split()[1]): np.array(l.split()[2:], np.float32) for l in out if l.startswith("S ")}
     for i, e in enumerate(envs):
         np.testing.assert_array_equal(states[i], e.obs())
+
+
+@pytest.mark.gpu
+def test_mirror_saves_reference_weights_files(tmp_path, wk):
+    """PPOAgent.Save (PPOAgent.cs:192-213): <FilePath>Data/Weights/{critic,actor}.weights"""
+    exe = build_mirror(tmp_path, wk)
+    root = str(tmp_path) + "/"
+    subprocess.run([exe, "4", "1", "actions", root], capture_output=True, text=True, check=True,
+                   timeout=120)
+    critic = (tmp_path / "Data" / "Weights" / "critic.weights").read_text(encoding="utf-8")
+    actor = (tmp_path / "Data" / "Weights" / "actor.weights").read_text(encoding="utf-8")
+    assert critic.startswith("Input |64| (LeakyReLU) |1| Output\n")
+    p = wk.parse_weights(critic, actor)
+    assert critic == wk.format_weights(p)[0] and np.isfinite(p).all()
