@@ -108,6 +108,19 @@ typedef struct wk_config {
                                (2 from 32,768 walkers, else 16) */
 } wk_config;
 
+/* The host-only fields of the reference's JSON configuration (SerializableHyperparameters,
+ * Hyperparameters.cs:11-77), plus storage for the network DSL strings that
+ * wk_config_from_json points wk_config at.  Not used by the kernels. */
+typedef struct wk_host_settings {
+  int CollectData;                /* 1 */
+  int SaveWeights;                /* 1 */
+  char CriticNeuralNetwork[256];  /* "Input |64| (LeakyReLU) |1| Output" */
+  char ActorNeuralNetwork[256];   /* "Input |64| (LeakyReLU) |64| (LeakyReLU) |4| (TanH) Output" */
+  char CriticWeightFileName[256]; /* "critic" */
+  char ActorWeightFileName[256];  /* "actor" */
+  char FilePath[1024];            /* AppDomain BaseDirectory: the executable's directory + "/" */
+} wk_host_settings;
+
 /* canonical per-env state dump: WK_STATE_FLOATS floats per env (identical layout to
  * the oracle's orc_env_dump).  Body b in {LLL, LLU, BODY, RLL, RLU} at b*20:
  * verts x0,y0..x5,y5 (BODY uses 5), centroid x,y, v x,y, w, angle, collided, pad. */
@@ -202,6 +215,22 @@ int wk_get_weights(wk_ctx* ctx, float* params /* WK_NPARAM */);
 int wk_set_weights(wk_ctx* ctx, const float* params);
 int wk_get_adam(wk_ctx* ctx, float* m, float* v, int* t);
 int wk_set_adam(wk_ctx* ctx, const float* m, const float* v, int t);
+
+/* JSON configuration files (replaces Hyperparameters.SerializeJson / DeserializeJson,
+ * Hyperparameters.cs:124-187, System.Text.Json default options, WriteIndented on save).
+ * wk_config_to_json: NULL cfg / host = defaults; returns -(bytes needed) when cap is too
+ * small.  wk_config_from_json: the document updates *cfg and *host in place (missing
+ * properties keep their values); a malformed document or a value outside
+ * ValidateHyperparameterValues (:189-217) returns WK_ERR_CONFIG and changes nothing;
+ * otherwise returns the number of ValidateVariables (:240-290) corrections (invalid file
+ * path / weights file names / network strings reset to defaults), their messages (one per
+ * line) in wk_last_error(NULL).  cfg's network-string pointers are set to host's buffers.
+ * No device is touched. */
+void wk_host_settings_defaults(wk_host_settings* host);
+int wk_config_to_json(const wk_config* cfg, const wk_host_settings* host, char* out, size_t cap);
+int wk_config_from_json(const char* json, wk_config* cfg, wk_host_settings* host);
+int wk_config_save_json(const char* path, const wk_config* cfg, const wk_host_settings* host);
+int wk_config_load_json(const char* path, wk_config* cfg, wk_host_settings* host);
 
 /* Weights files in the reference's text format (replaces PPOAgent.Save / Load,
  * PPOAgent.cs:192-213, over NeuralNetwork.Save / Load NeuralNetwork.cs:94-176,

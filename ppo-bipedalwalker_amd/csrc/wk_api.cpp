@@ -19,11 +19,15 @@
 #include "../../include/wk_api.h"
 #include "wk_common.h"
 #include "wk_kernels.h"
+#include "wk_text.h"
 
 
 static const char* kCriticDefault = "Input |64| (LeakyReLU) |1| Output";
 static const char* kActorDefault = "Input |64| (LeakyReLU) |64| (LeakyReLU) |4| (TanH) Output";
 static thread_local std::string g_create_error;
+namespace wk {
+void set_last_error(const std::string& msg) { g_create_error = msg; }
+}  // namespace wk
 
 // level 1: one event pair per rollout / returns / whole PPO update (cheap enough for a
 // timed loop); level 2 adds one per gradient / reduce / all-reduce / Adam launch
@@ -180,6 +184,7 @@ const char* wk_last_error(const wk_ctx* ctx) {
 static int validate(const wk_config* c, std::string& why) {
   char b[256];
   auto bad = [&](const char* m) { why = m; return WK_ERR_CONFIG; };
+  if (c->GameSpeed <= 0 || c->GameSpeed >= 10) return bad("Invalid game speed, should be in range 0<x<10");
   if (c->Iterations <= 0 || c->Iterations >= 200) return bad("Invalid iterations count, should be in range 0<x<200");
   if (c->MaxTimesteps <= 0) return bad("Invalid maximum time steps amount, should be in range x>0");
   if (c->Alpha <= 0 || c->Alpha >= 10) return bad("Invalid alpha value, should be in range 0<x<10");
@@ -892,57 +897,14 @@ const DenseSpec kActorLayers[] = {{wk::OFF_A_W1, 64, 12, wk::OFF_A_B1},
                                   {wk::OFF_A_W2, 64, 64, wk::OFF_A_B2},
                                   {wk::OFF_A_W3, 4, 64, wk::OFF_A_B3}};
 
-std::string dotnet_float(float v) {
-  if (std::isnan(v)) return "NaN";
-  if (std::isinf(v)) return v > 0 ? "\xe2\x88\x9e" : "-\xe2\x88\x9e";  // .NET Core 3.0+: "∞"
-  if (v == 0.0f) return std::signbit(v) ? "-0" : "0";
-  char buf[64];
-  int prec = 1;
-  for (; prec <= 9; prec++) {  // shortest round-trip significant digits
-    snprintf(buf, sizeof buf, "%.*e", prec - 1, (double)v);
-    if (strtof(buf, nullptr) == v) break;
-  }
-  // buf = "[-]d.ddde[+-]XX": split mantissa digits and exponent
-  std::string s(buf);
-  const size_t epos = s.find('e');
-  const int exp10 = atoi(s.c_str() + epos + 1);
-  std::string mant = s.substr(0, epos);
-  const bool neg = mant[0] == '-';
-  if (neg) mant = mant.substr(1);
-  std::string digits;
-  for (char ch : mant)
-    if (ch != '.') digits += ch;
-  while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
-  std::string out = neg ? "-" : "";
-  // Number.Formatting FormatGeneral: scientific when the decimal-point position
-  // (exp10 + 1) exceeds max(digit count, SinglePrecision = 9) or is below -3
-  const int scale = exp10 + 1;
-  if (scale > std::max((int)digits.size(), 9) || scale < -3) {  // d[.ddd]E+XX
-    out += digits[0];
-    if (digits.size() > 1) out += "." + digits.substr(1);
-    char eb[16];
-    snprintf(eb, sizeof eb, "E%c%02d", exp10 < 0 ? '-' : '+', exp10 < 0 ? -exp10 : exp10);
-    out += eb;
-  } else if (exp10 < 0) {
-    out += "0." + std::string(-exp10 - 1, '0') + digits;
-  } else {
-    if ((int)digits.size() <= exp10 + 1) {
-      out += digits + std::string(exp10 + 1 - digits.size(), '0');
-    } else {
-      out += digits.substr(0, exp10 + 1) + "." + digits.substr(exp10 + 1);
-    }
-  }
-  return out;
-}
-
 std::string format_network(const float* p, const char* dsl, const DenseSpec* layers, int nl) {
   std::string text = std::string(dsl) + "\n";
   for (int l = 0; l < nl; l++) {
     const DenseSpec& d = layers[l];
     std::string line = "W";
-    for (int i = 0; i < d.rows * d.cols; i++) line += " " + dotnet_float(p[d.off_w + i]);
+    for (int i = 0; i < d.rows * d.cols; i++) line += " " + wk::dotnet_float(p[d.off_w + i]);
     line += " B";
-    for (int i = 0; i < d.rows; i++) line += " " + dotnet_float(p[d.off_b + i]);
+    for (int i = 0; i < d.rows; i++) line += " " + wk::dotnet_float(p[d.off_b + i]);
     text += line + "\n";
   }
   return text;

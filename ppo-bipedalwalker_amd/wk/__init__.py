@@ -32,6 +32,8 @@ EXPORTS = [
     "wk_set_trajectory", "wk_compute_returns", "wk_ppo_update", "wk_train_batch",
     "wk_minibatch_gradient", "wk_save_weights", "wk_load_weights", "wk_format_weights",
     "wk_parse_weights", "wk_checkpoint_save", "wk_checkpoint_load",
+    "wk_host_settings_defaults", "wk_config_to_json", "wk_config_from_json",
+    "wk_config_save_json", "wk_config_load_json",
     "wk_comm_unique_id", "wk_comm_init", "wk_allreduce_test", "wk_profile_enable",
     "wk_profile_get", "wk_profile_reset",
 ]
@@ -50,6 +52,16 @@ class WkConfig(C.Structure):
         ("Minibatch", C.c_int), ("MinibatchGlobal", C.c_int), ("EnvOffset", C.c_int),
         ("RandomizeStart", C.c_int), ("RandomizeMaterial", C.c_int),
         ("LanesPerWalker", C.c_int),
+    ]
+
+
+class HostSettings(C.Structure):
+    """wk_host_settings: SerializableHyperparameters' host-only fields (Hyperparameters.cs:11-77)."""
+    _fields_ = [
+        ("CollectData", C.c_int), ("SaveWeights", C.c_int),
+        ("CriticNeuralNetwork", C.c_char * 256), ("ActorNeuralNetwork", C.c_char * 256),
+        ("CriticWeightFileName", C.c_char * 256), ("ActorWeightFileName", C.c_char * 256),
+        ("FilePath", C.c_char * 1024),
     ]
 
 
@@ -161,6 +173,11 @@ def load_library(path=None):
         "wk_parse_weights": (I, [C.c_char_p, C.c_char_p, P]),
         "wk_checkpoint_save": (I, [P, C.c_char_p]),
         "wk_checkpoint_load": (I, [P, C.c_char_p]),
+        "wk_host_settings_defaults": (None, [C.POINTER(HostSettings)]),
+        "wk_config_to_json": (I, [C.POINTER(WkConfig), C.POINTER(HostSettings), C.c_char_p, C.c_size_t]),
+        "wk_config_from_json": (I, [C.c_char_p, C.POINTER(WkConfig), C.POINTER(HostSettings)]),
+        "wk_config_save_json": (I, [C.c_char_p, C.POINTER(WkConfig), C.POINTER(HostSettings)]),
+        "wk_config_load_json": (I, [C.c_char_p, C.POINTER(WkConfig), C.POINTER(HostSettings)]),
         "wk_comm_unique_id": (I, [P]),
         "wk_comm_init": (I, [P, I, I, P]),
         "wk_allreduce_test": (I, [P, P, I]),
@@ -204,6 +221,44 @@ def default_config(**overrides):
             v = v.encode()
         setattr(c, k, v)
     return c
+
+
+def default_host_settings():
+    h = HostSettings()
+    load_library().wk_host_settings_defaults(C.byref(h))
+    return h
+
+
+def config_to_json(cfg=None, host=None):
+    """Hyperparameters.SerializeJson (Hyperparameters.cs:124-131): the indented JSON text."""
+    lib = load_library()
+    cp = None if cfg is None else C.byref(cfg)
+    hp = None if host is None else C.byref(host)
+    need = -lib.wk_config_to_json(cp, hp, None, 0)
+    if need <= 0:
+        raise WkError(f"wk_config_to_json: {lib.wk_last_error(None).decode()}")
+    buf = C.create_string_buffer(need)
+    rc = lib.wk_config_to_json(cp, hp, buf, need)
+    if rc != 0:
+        raise WkError(f"wk_config_to_json failed ({rc}): {lib.wk_last_error(None).decode()}")
+    return buf.value.decode()
+
+
+def config_from_json(text, cfg=None, host=None):
+    """Hyperparameters.DeserializeJson (Hyperparameters.cs:135-187) applied to (cfg, host)
+    (defaults when None).  Returns (cfg, host, corrections): corrections lists the
+    ValidateVariables messages (values reset to defaults).  Raises WkError when the
+    document is malformed or a value is out of range (nothing is changed then)."""
+    lib = load_library()
+    cfg = default_config() if cfg is None else cfg
+    host = default_host_settings() if host is None else host
+    raw = text.encode() if isinstance(text, str) else bytes(text)
+    rc = lib.wk_config_from_json(raw, C.byref(cfg), C.byref(host))
+    msg = lib.wk_last_error(None).decode()
+    if rc < 0:
+        raise WkError(f"wk_config_from_json failed ({rc}): {msg}")
+    cfg._host = host  # cfg's network strings point into host's buffers
+    return cfg, host, (msg.split("\n") if rc > 0 else [])
 
 
 def format_weights(params):

@@ -93,6 +93,41 @@ def test_shortest_digits_agree_with_numpy(wk):
         assert np.float32(tok) == v
 
 
+def _tokens(wk, p):
+    critic, actor = wk.format_weights(p)
+    toks = []
+    for text in (critic, actor):
+        for line in text.split("\n")[1:-1]:
+            toks += [t for t in line.split(" ") if t not in ("W", "B")]
+    order = np.concatenate([np.concatenate([np.r_[w.ravel(), b] for w, b in net])
+                            for net in _layout(wk, np.arange(wk.NPARAM, dtype=np.float64))])
+    out = [None] * wk.NPARAM
+    for tok, idx in zip(toks, order.astype(np.int64)):
+        out[idx] = tok
+    return out
+
+
+def test_shortest_digits_at_binade_edges(wk):
+    """Powers of two (asymmetric round-trip interval) and their neighbours, normal and
+    subnormal: the digits equal numpy's shortest unique repr (Dragon4)."""
+    ex = np.arange(1, 255, dtype=np.uint32) << 23
+    sub = np.uint32(1) << np.arange(23, dtype=np.uint32)
+    base = np.concatenate([ex, sub])
+    bits = np.concatenate([base, base + 1, base - 1, base | 0x80000000])
+    bits = bits[(bits & 0x7F800000) != 0x7F800000]
+    p = np.ones(wk.NPARAM, np.float32)
+    p[:bits.size] = bits.view(np.float32)
+    toks = _tokens(wk, p)
+    for i in range(bits.size):
+        v = p[i]
+        sci = np.format_float_scientific(v, unique=True, trim="-")
+        mant, e = sci.split("e")
+        tok = toks[i]
+        assert np.float32(tok) == v, (tok, sci)
+        digits = tok.lstrip("-").split("E")[0].replace(".", "").lstrip("0").rstrip("0")
+        assert digits == mant.lstrip("-").replace(".", "").rstrip("0"), (tok, sci)
+
+
 def test_round_trip_bitexact(wk):
     rng = np.random.default_rng(3)
     bits = rng.integers(0, 2**32, wk.NPARAM, dtype=np.uint64).astype(np.uint32)
