@@ -174,6 +174,15 @@ typedef struct wk_rollout_stats {
   int32_t pad;
 } wk_rollout_stats;
 
+/* one finished episode (data collection) */
+typedef struct wk_episode_rec {
+  float total_reward;  /* (float) of the double sum of its rewards, like Enumerable.Sum */
+  int32_t env;         /* global walker id (EnvOffset + index) */
+  int32_t length;      /* env-steps in the episode */
+  uint32_t step;       /* env-step it finished at, counted over this context's wk_rollout
+                          calls (equal across ranks stepping in lockstep) */
+} wk_episode_rec;
+
 /* kernel timing (HIP events on the context's stream), cumulative since last reset */
 typedef struct wk_profile {
   double physics_ms;   int64_t physics_launches;  int64_t physics_env_steps;
@@ -248,8 +257,9 @@ int wk_format_weights(const float* params, char* critic_text, size_t critic_cap,
 int wk_parse_weights(const char* critic_text, const char* actor_text, float* params);
 
 /* Binary checkpoint for bit-exact resume (new; the reference persists only weights):
- * weights, Adam m / v / t, every walker record, Philox step counters, start offsets and
- * materials.  Loading requires the same n_env, seed and EnvOffset; it invalidates the
+ * weights, Adam m / v / t, every walker record, Philox step counters, start offsets,
+ * materials, running episode rewards / lengths and the episode-log clock (the episode and
+ * loss logs are not included: drain them first).  Loading requires the same n_env, seed and EnvOffset; it invalidates the
  * trajectory buffer (roll out again before wk_ppo_update). */
 int wk_checkpoint_save(wk_ctx* ctx, const char* path);
 int wk_checkpoint_load(wk_ctx* ctx, const char* path);
@@ -280,6 +290,25 @@ int wk_minibatch_gradient(wk_ctx* ctx, int B, float b_div, const float* states,
                           const float* actions, const float* logp_old, const float* returns,
                           const float* adv, float* critic_diag, float* actor_diag,
                           float* grads_out, int* skipped);
+
+/* Data collection (replaces ConsoleRenderer.AddTotalEpisodeReward / AddCriticLoss /
+ * AddActorLoss, ConsoleRenderer.cs:79-95, fed by PPOAgent.Train PPOAgent.cs:151,165-166,
+ * and CreateDataFile :124-135).  On by default (Hyperparameters.CollectData = true): every
+ * wk_rollout appends each finished episode to a device log in completion order
+ * (env-step, walker) -- wk_step does not feed it -- and every wk_ppo_update appends its last minibatch's
+ * (critic, actor) diagnostics.  The episode log holds n_env * Horizon records and the loss
+ * log 65,536 updates; drain them at least that often (the overflow is counted in
+ * *dropped).  Drains clear the logs; a cap smaller than the held count is WK_ERR_ARG. */
+int wk_collect_data(wk_ctx* ctx, int on);
+int wk_episode_log_count(wk_ctx* ctx, int64_t* episodes, int64_t* updates);
+int wk_episode_log_drain(wk_ctx* ctx, wk_episode_rec* out, int64_t cap, int64_t* n_out,
+                         int64_t* dropped);
+int wk_loss_log_drain(wk_ctx* ctx, float* critic, float* actor, int64_t cap, int64_t* n_out,
+                      int64_t* dropped);
+/* the reference's data file: rewards / critic losses / actor losses lists, no device */
+int wk_write_data_file(const char* path, const float* total_rewards, int64_t n_rewards,
+                       const float* critic_losses, int64_t n_critic, const float* actor_losses,
+                       int64_t n_actor);
 
 /* multi-GPU: RCCL communicator over the ranks' contexts (one per GPU) */
 int wk_comm_unique_id(uint8_t* id /* 128 bytes */);

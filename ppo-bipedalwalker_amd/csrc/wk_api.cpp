@@ -56,6 +56,18 @@ struct wk_ctx {
   float *ts = nullptr, *ta = nullptr, *tlp = nullptr, *tr = nullptr, *tv = nullptr, *tret = nullptr, *tadv = nullptr;
   uint8_t* td = nullptr;
   bool returns_valid = false;
+  // data collection (ConsoleRenderer.AddTotalEpisodeReward / AddCriticLoss / AddActorLoss)
+  int collect = 1;
+  uint32_t rollout_steps = 0;  // env-steps taken by wk_rollout so far (episode log clock)
+  double* ep_acc = nullptr;       // [n] running episode reward
+  int32_t* ep_len = nullptr;      // [n]
+  void* ep_scratch = nullptr;     // [T][n] float2
+  uint32_t* ep_rowcnt = nullptr;  // [T]
+  uint64_t* ep_count = nullptr;   // device: records appended since the last drain
+  wk::EpisodeRecDev* ep_log = nullptr;
+  uint64_t ep_cap = 0;
+  float* loss_log = nullptr;      // [loss_cap][2] (critic, actor) per PPO update
+  uint64_t loss_count = 0, loss_cap = 0;
   // scratch
   float* partial = nullptr; size_t partial_floats = 0;
   void* scratch = nullptr; size_t scratch_bytes = 0;
@@ -290,6 +302,15 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   ALLOC(x->tret, sizeof(float) * n * T);
   ALLOC(x->tadv, sizeof(float) * n * T);
   ALLOC(x->td, n * T);
+  x->ep_cap = (uint64_t)n * T;  // one rollout's worst case: every env-step ends an episode
+  x->loss_cap = 1u << 16;
+  ALLOC(x->ep_acc, sizeof(double) * n);
+  ALLOC(x->ep_len, sizeof(int32_t) * n);
+  ALLOC(x->ep_scratch, sizeof(float) * 2 * n * T);
+  ALLOC(x->ep_rowcnt, sizeof(uint32_t) * T);
+  ALLOC(x->ep_count, sizeof(uint64_t));
+  ALLOC(x->ep_log, sizeof(wk::EpisodeRecDev) * x->ep_cap);
+  ALLOC(x->loss_log, sizeof(float) * 2 * x->loss_cap);
 #undef ALLOC
   // synthetic randomisation of the initial state (BASELINE.json config 2 / 5)
   std::vector<float> dx(n, 0.0f);
@@ -304,7 +325,11 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
       hipMemset(x->rng_t, 0, sizeof(uint32_t) * n) != hipSuccess ||
       hipMemset(x->m, 0, sizeof(float) * wk::NPARAM) != hipSuccess ||
       hipMemset(x->v, 0, sizeof(float) * wk::NPARAM) != hipSuccess ||
-      hipMemset(x->td, 0, n * T) != hipSuccess) {
+      hipMemset(x->td, 0, n * T) != hipSuccess ||
+      hipMemset(x->ep_acc, 0, sizeof(double) * n) != hipSuccess ||
+      hipMemset(x->ep_len, 0, sizeof(int32_t) * n) != hipSuccess ||
+      hipMemset(x->ep_rowcnt, 0, sizeof(uint32_t) * T) != hipSuccess ||
+      hipMemset(x->ep_count, 0, sizeof(uint64_t)) != hipSuccess) {
     x->err = "initial upload failed";
     return fail(WK_ERR_HIP);
   }
@@ -326,7 +351,9 @@ int wk_destroy(wk_ctx* c) {
   for (auto e : c->pool) (void)hipEventDestroy(e);
   if (c->comm) ncclCommDestroy(c->comm);
   void* bufs[] = {c->st, c->dxoff, c->mat, c->rng_t, c->W, c->Wz, c->m, c->v, c->grad, c->ts, c->ta,
-                  c->tlp, c->tr, c->tv, c->tret, c->tadv, c->td, c->partial, c->scratch, c->scratch2};
+                  c->tlp, c->tr, c->tv, c->tret, c->tadv, c->td, c->partial, c->scratch, c->scratch2,
+                  c->ep_acc, c->ep_len, c->ep_scratch, c->ep_rowcnt, c->ep_count, c->ep_log,
+                  c->loss_log};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -352,6 +379,7 @@ int wk_reset(wk_ctx* c, const uint8_t* mask) {
   }
   // Environment.Reset re-creates the walker after the floor (post-reset body order)
   HIPCHK(c, wk::launch_env_init(c->P, c->st, c->dxoff, dmask, 1, c->stream));
+  HIPCHK(c, wk::launch_episode_reset(c->n, dmask, c->ep_acc, c->ep_len, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return WK_OK;
 }
@@ -585,6 +613,14 @@ int wk_rollout(wk_ctx* c, int horizon) {
     HIPCHK(c, wk::launch_env_step(3, c->P, A, c->stream));
   }
   c->T_valid = horizon;
+  if (c->collect) {
+    wk::EpisodeArgs e{c->n, horizon, c->cfg.EnvOffset, c->rollout_steps, c->tr, c->td, c->ep_acc,
+                      c->ep_len, (float2*)c->ep_scratch, c->ep_rowcnt, c->ep_count, c->ep_cap,
+                      c->ep_log};
+    ProfScope ps(c, PK_RET);
+    HIPCHK(c, wk::launch_episode_log(e, c->stream));
+  }
+  c->rollout_steps += (uint32_t)horizon;
   return returns_impl(c);
 }
 
@@ -720,6 +756,12 @@ int wk_ppo_update(wk_ctx* c, const wk_ppo_args* args, float* critic_diag, float*
     ProfScope ps(c, PK_UPDATE);
     int r = ppo_update_impl(c, args);
     if (r) return r;
+  }
+  if (c->collect) {  // the last minibatch's losses, as PPOAgent.Train hands them on (:165-166)
+    if (c->loss_count < c->loss_cap)
+      HIPCHK(c, hipMemcpyAsync(c->loss_log + 2 * c->loss_count, c->grad + wk::NPARAM,
+                               2 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+    c->loss_count++;
   }
   if (!critic_diag && !actor_diag) return WK_OK;  // stays asynchronous on the stream
   float diag[3] = {0, 0, 0};
@@ -975,8 +1017,15 @@ const uint32_t kCkptMagic = 0x4B434B57u;  // "WKCK"
 struct CkptHeader {
   uint32_t magic, version, n_env, nstate, nparam, adam_t;
   uint64_t seed;
-  int32_t env_offset, iterations, max_timesteps, pad;
+  int32_t env_offset, iterations, max_timesteps;
+  uint32_t rollout_steps;
 };
+static_assert(sizeof(CkptHeader) == 48, "checkpoint header");
+const uint32_t kCkptVersion = 2;
+size_t ckpt_bytes(size_t n) {
+  return sizeof(CkptHeader) + sizeof(float) * (3 * wk::NPARAM + n * wk::NSTATE + 2 * n) +
+         sizeof(int32_t) * n + sizeof(double) * n + sizeof(int32_t) * n;
+}
 }  // namespace
 
 extern "C" {
@@ -1038,11 +1087,10 @@ int wk_load_weights(wk_ctx* c, const char* critic_path, const char* actor_path) 
 int wk_checkpoint_save(wk_ctx* c, const char* path) {
   if (!c || !path) return WK_ERR_ARG;
   const size_t n = c->n;
-  CkptHeader h{kCkptMagic, 1u, (uint32_t)n, (uint32_t)wk::NSTATE, (uint32_t)wk::NPARAM,
+  CkptHeader h{kCkptMagic, kCkptVersion, (uint32_t)n, (uint32_t)wk::NSTATE, (uint32_t)wk::NPARAM,
                (uint32_t)c->adam_t, c->seed, c->cfg.EnvOffset, c->cfg.Iterations,
-               c->cfg.MaxTimesteps, 0};
-  std::vector<char> buf(sizeof h + sizeof(float) * (3 * wk::NPARAM + n * wk::NSTATE + 2 * n) +
-                        sizeof(int32_t) * n);
+               c->cfg.MaxTimesteps, c->rollout_steps};
+  std::vector<char> buf(ckpt_bytes(n));
   char* q = buf.data();
   memcpy(q, &h, sizeof h); q += sizeof h;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1052,7 +1100,9 @@ int wk_checkpoint_save(wk_ctx* c, const char* path) {
   HIPCHK(c, hipMemcpy(q, c->st, sizeof(float) * n * wk::NSTATE, hipMemcpyDeviceToHost)); q += sizeof(float) * n * wk::NSTATE;
   HIPCHK(c, hipMemcpy(q, c->rng_t, sizeof(uint32_t) * n, hipMemcpyDeviceToHost)); q += sizeof(uint32_t) * n;
   HIPCHK(c, hipMemcpy(q, c->dxoff, sizeof(float) * n, hipMemcpyDeviceToHost)); q += sizeof(float) * n;
-  HIPCHK(c, hipMemcpy(q, c->mat, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(q, c->mat, sizeof(int32_t) * n, hipMemcpyDeviceToHost)); q += sizeof(int32_t) * n;
+  HIPCHK(c, hipMemcpy(q, c->ep_acc, sizeof(double) * n, hipMemcpyDeviceToHost)); q += sizeof(double) * n;
+  HIPCHK(c, hipMemcpy(q, c->ep_len, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
   if (!write_file(path, buf.data(), buf.size())) { SETERR(c, "cannot write checkpoint '%s'", path); return WK_ERR_ARG; }
   return WK_OK;
 }
@@ -1065,8 +1115,8 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
   CkptHeader h;
   if (data.size() < sizeof h) { SETERR(c, "checkpoint '%s' truncated", path); return WK_ERR_ARG; }
   memcpy(&h, data.data(), sizeof h);
-  const size_t need = sizeof h + sizeof(float) * (3 * wk::NPARAM + n * wk::NSTATE + 2 * n) + sizeof(int32_t) * n;
-  if (h.magic != kCkptMagic || h.version != 1u) { SETERR(c, "'%s' is not a wk checkpoint", path); return WK_ERR_ARG; }
+  const size_t need = ckpt_bytes(n);
+  if (h.magic != kCkptMagic || h.version != kCkptVersion) { SETERR(c, "'%s' is not a wk checkpoint", path); return WK_ERR_ARG; }
   if (h.n_env != n || h.nstate != (uint32_t)wk::NSTATE || h.nparam != (uint32_t)wk::NPARAM || data.size() != need) {
     SETERR(c, "checkpoint '%s' is for %u walkers (context has %zu)", path, h.n_env, n);
     return WK_ERR_ARG;
@@ -1084,12 +1134,103 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
   HIPCHK(c, hipMemcpy(c->st, q, sizeof(float) * n * wk::NSTATE, hipMemcpyHostToDevice)); q += sizeof(float) * n * wk::NSTATE;
   HIPCHK(c, hipMemcpy(c->rng_t, q, sizeof(uint32_t) * n, hipMemcpyHostToDevice)); q += sizeof(uint32_t) * n;
   HIPCHK(c, hipMemcpy(c->dxoff, q, sizeof(float) * n, hipMemcpyHostToDevice)); q += sizeof(float) * n;
-  HIPCHK(c, hipMemcpy(c->mat, q, sizeof(int32_t) * n, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->mat, q, sizeof(int32_t) * n, hipMemcpyHostToDevice)); q += sizeof(int32_t) * n;
+  HIPCHK(c, hipMemcpy(c->ep_acc, q, sizeof(double) * n, hipMemcpyHostToDevice)); q += sizeof(double) * n;
+  HIPCHK(c, hipMemcpy(c->ep_len, q, sizeof(int32_t) * n, hipMemcpyHostToDevice));
   c->adam_t = (int)h.adam_t;
+  c->rollout_steps = h.rollout_steps;
   c->T_valid = 0;
   c->returns_valid = 0;
   HIPCHK(c, wk::launch_swizzle(c->W, c->Wz, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return WK_OK;
+}
+
+
+// ---------------- data collection ----------------
+static_assert(sizeof(wk_episode_rec) == sizeof(wk::EpisodeRecDev), "episode record layout");
+
+int wk_collect_data(wk_ctx* c, int on) {
+  if (!c) return WK_ERR_ARG;
+  c->collect = on ? 1 : 0;
+  return WK_OK;
+}
+
+int wk_episode_log_count(wk_ctx* c, int64_t* episodes, int64_t* updates) {
+  if (!c) return WK_ERR_ARG;
+  uint64_t cnt = 0;
+  HIPCHK(c, hipMemcpyAsync(&cnt, c->ep_count, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (episodes) *episodes = (int64_t)cnt;
+  if (updates) *updates = (int64_t)c->loss_count;
+  return WK_OK;
+}
+
+int wk_episode_log_drain(wk_ctx* c, wk_episode_rec* out, int64_t cap, int64_t* n_out,
+                         int64_t* dropped) {
+  if (!c || cap < 0 || (cap > 0 && !out)) return WK_ERR_ARG;
+  uint64_t cnt = 0;
+  HIPCHK(c, hipMemcpyAsync(&cnt, c->ep_count, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint64_t kept = cnt < c->ep_cap ? cnt : c->ep_cap;
+  if ((uint64_t)cap < kept) {
+    SETERR(c, "episode log holds %llu records, buffer has room for %lld", (unsigned long long)kept, (long long)cap);
+    return WK_ERR_ARG;
+  }
+  if (kept) HIPCHK(c, hipMemcpy(out, c->ep_log, sizeof(wk_episode_rec) * kept, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemsetAsync(c->ep_count, 0, sizeof(uint64_t), c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (n_out) *n_out = (int64_t)kept;
+  if (dropped) *dropped = (int64_t)(cnt - kept);
+  return WK_OK;
+}
+
+int wk_loss_log_drain(wk_ctx* c, float* critic, float* actor, int64_t cap, int64_t* n_out,
+                      int64_t* dropped) {
+  if (!c || cap < 0 || (cap > 0 && (!critic || !actor))) return WK_ERR_ARG;
+  const uint64_t kept = c->loss_count < c->loss_cap ? c->loss_count : c->loss_cap;
+  if ((uint64_t)cap < kept) {
+    SETERR(c, "loss log holds %llu updates, buffer has room for %lld", (unsigned long long)kept, (long long)cap);
+    return WK_ERR_ARG;
+  }
+  std::vector<float> buf(2 * kept);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (kept) HIPCHK(c, hipMemcpy(buf.data(), c->loss_log, sizeof(float) * 2 * kept, hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < kept; i++) {
+    critic[i] = buf[2 * i];
+    actor[i] = buf[2 * i + 1];
+  }
+  if (n_out) *n_out = (int64_t)kept;
+  if (dropped) *dropped = (int64_t)(c->loss_count - kept);
+  c->loss_count = 0;
+  return WK_OK;
+}
+
+// ConsoleRenderer.CreateDataFile (ConsoleRenderer.cs:124-135): three space-joined float
+// lists (float.ToString(), en-US) each followed by a "length N, <name>" line and a blank line
+int wk_write_data_file(const char* path, const float* total_rewards, int64_t n_rewards,
+                       const float* critic_losses, int64_t n_critic, const float* actor_losses,
+                       int64_t n_actor) {
+  if (!path || n_rewards < 0 || n_critic < 0 || n_actor < 0 ||
+      (n_rewards && !total_rewards) || (n_critic && !critic_losses) || (n_actor && !actor_losses)) {
+    g_create_error = "invalid argument";
+    return WK_ERR_ARG;
+  }
+  std::string data;
+  auto list = [&](const float* v, int64_t k, const char* name) {
+    for (int64_t i = 0; i < k; i++) {
+      if (i) data += ' ';
+      data += wk::dotnet_float(v[i]);
+    }
+    data += "\nlength " + std::to_string(k) + ", " + name + "\n\n";
+  };
+  list(total_rewards, n_rewards, "total rewards");
+  list(critic_losses, n_critic, "critic losses");
+  list(actor_losses, n_actor, "actor losses");
+  if (!write_file(path, data.data(), data.size())) {
+    g_create_error = std::string("cannot write '") + path + "'";
+    return WK_ERR_ARG;
+  }
   return WK_OK;
 }
 

@@ -95,4 +95,29 @@ hipError_t launch_adam(const AdamArgs& a, hipStream_t s);
 hipError_t launch_normalize(float* x, int n, float eps, hipStream_t s);
 hipError_t launch_xavier(float* W, uint64_t seed, hipStream_t s);
 
+// data collection: per-episode totals of a recorded rollout appended to the device log;
+// layout == wk_episode_rec (include/wk_api.h)
+struct EpisodeRecDev {
+  float total_reward;
+  int32_t env;
+  int32_t length;
+  uint32_t step;
+};
+struct EpisodeArgs {
+  int n, T, env_offset;
+  uint32_t step0;             // rollout env-steps taken before this one
+  const float* rewards;      // [T][n]
+  const uint8_t* dones;      // [T][n]
+  double* acc;               // [n] running episode reward (carried across rollouts)
+  int32_t* len;              // [n] running episode length
+  float2* scratch;           // [T][n] (total, length bits), written where done
+  uint32_t* row_cnt;         // [T], zero on entry and exit
+  uint64_t* log_count;       // records appended so far (may exceed cap: dropped)
+  uint64_t cap;
+  EpisodeRecDev* log;
+};
+hipError_t launch_episode_log(const EpisodeArgs& a, hipStream_t s);
+hipError_t launch_episode_reset(int n, const uint8_t* mask, double* acc, int32_t* len,
+                                hipStream_t s);
+
 }  // namespace wk

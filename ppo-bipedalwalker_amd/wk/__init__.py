@@ -33,7 +33,8 @@ EXPORTS = [
     "wk_minibatch_gradient", "wk_save_weights", "wk_load_weights", "wk_format_weights",
     "wk_parse_weights", "wk_checkpoint_save", "wk_checkpoint_load",
     "wk_host_settings_defaults", "wk_config_to_json", "wk_config_from_json",
-    "wk_config_save_json", "wk_config_load_json",
+    "wk_config_save_json", "wk_config_load_json", "wk_collect_data", "wk_episode_log_count",
+    "wk_episode_log_drain", "wk_loss_log_drain", "wk_write_data_file",
     "wk_comm_unique_id", "wk_comm_init", "wk_allreduce_test", "wk_profile_enable",
     "wk_profile_get", "wk_profile_reset",
 ]
@@ -63,6 +64,15 @@ class HostSettings(C.Structure):
         ("CriticWeightFileName", C.c_char * 256), ("ActorWeightFileName", C.c_char * 256),
         ("FilePath", C.c_char * 1024),
     ]
+
+
+class EpisodeRec(C.Structure):
+    _fields_ = [("total_reward", C.c_float), ("env", C.c_int32), ("length", C.c_int32),
+                ("step", C.c_uint32)]
+
+
+EPISODE_DTYPE = np.dtype([("total_reward", np.float32), ("env", np.int32), ("length", np.int32),
+                          ("step", np.uint32)])
 
 
 class PairTrace(C.Structure):
@@ -178,6 +188,11 @@ def load_library(path=None):
         "wk_config_from_json": (I, [C.c_char_p, C.POINTER(WkConfig), C.POINTER(HostSettings)]),
         "wk_config_save_json": (I, [C.c_char_p, C.POINTER(WkConfig), C.POINTER(HostSettings)]),
         "wk_config_load_json": (I, [C.c_char_p, C.POINTER(WkConfig), C.POINTER(HostSettings)]),
+        "wk_collect_data": (I, [P, I]),
+        "wk_episode_log_count": (I, [P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+        "wk_episode_log_drain": (I, [P, P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+        "wk_loss_log_drain": (I, [P, P, P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+        "wk_write_data_file": (I, [C.c_char_p, P, C.c_int64, P, C.c_int64, P, C.c_int64]),
         "wk_comm_unique_id": (I, [P]),
         "wk_comm_init": (I, [P, I, I, P]),
         "wk_allreduce_test": (I, [P, P, I]),
@@ -259,6 +274,15 @@ def config_from_json(text, cfg=None, host=None):
         raise WkError(f"wk_config_from_json failed ({rc}): {msg}")
     cfg._host = host  # cfg's network strings point into host's buffers
     return cfg, host, (msg.split("\n") if rc > 0 else [])
+
+
+def write_data_file(path, total_rewards, critic_losses, actor_losses):
+    """ConsoleRenderer.CreateDataFile (ConsoleRenderer.cs:124-135)."""
+    lib = load_library()
+    r, c, a = (np.ascontiguousarray(x, np.float32) for x in (total_rewards, critic_losses, actor_losses))
+    rc = lib.wk_write_data_file(os.fsencode(path), _ptr(r), r.size, _ptr(c), c.size, _ptr(a), a.size)
+    if rc != 0:
+        raise WkError(f"wk_write_data_file failed ({rc}): {lib.wk_last_error(None).decode()}")
 
 
 def format_weights(params):
@@ -418,6 +442,35 @@ class Engine:
 
     def checkpoint_load(self, path):
         self._chk(self.lib.wk_checkpoint_load(self.h, os.fsencode(path)), "wk_checkpoint_load")
+
+    # -- data collection (ConsoleRenderer.AddTotalEpisodeReward / AddCriticLoss / AddActorLoss) --
+    def collect_data(self, on=True):
+        self._chk(self.lib.wk_collect_data(self.h, int(bool(on))), "wk_collect_data")
+
+    def episode_log_count(self):
+        e, u = C.c_int64(), C.c_int64()
+        self._chk(self.lib.wk_episode_log_count(self.h, C.byref(e), C.byref(u)), "wk_episode_log_count")
+        return e.value, u.value
+
+    def drain_episodes(self):
+        """finished episodes since the last drain (structured array EPISODE_DTYPE) and the
+        number dropped by overflow"""
+        cnt, _ = self.episode_log_count()
+        out = np.empty(cnt, EPISODE_DTYPE)
+        n, dropped = C.c_int64(), C.c_int64()
+        self._chk(self.lib.wk_episode_log_drain(self.h, _ptr(out) if cnt else None, cnt, C.byref(n),
+                                                C.byref(dropped)), "wk_episode_log_drain")
+        return out[:n.value], dropped.value
+
+    def drain_losses(self):
+        """(critic, actor) diagnostics of each PPO update since the last drain"""
+        _, cnt = self.episode_log_count()
+        cap = min(cnt, 1 << 16)
+        c, a = np.empty(cap, np.float32), np.empty(cap, np.float32)
+        n, dropped = C.c_int64(), C.c_int64()
+        self._chk(self.lib.wk_loss_log_drain(self.h, _ptr(c) if cap else None, _ptr(a) if cap else None,
+                                             cap, C.byref(n), C.byref(dropped)), "wk_loss_log_drain")
+        return c[:n.value], a[:n.value]
 
     def policy_sample(self, obs, env_ids=None, steps=None):
         obs = _f32(obs)

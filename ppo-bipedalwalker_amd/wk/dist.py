@@ -50,3 +50,16 @@ def broadcast_unique_id(uid_or_none, group=None):
         buf[:] = torch.tensor(list(uid_or_none), dtype=torch.uint8)
     dist.broadcast(buf, src=0, group=group)
     return bytes(buf.tolist())
+
+
+def gather_episode_log(recs, group=None):
+    """Cross-rank aggregation for the data file: every rank's drained episode records are
+    gathered to all ranks (torch.distributed, any backend) and merged in completion order
+    (env-step, global walker id) -- the order one context holding all walkers would log."""
+    import numpy as np
+    import torch.distributed as dist
+    from . import EPISODE_DTYPE
+    parts = [None] * dist.get_world_size(group)
+    dist.all_gather_object(parts, np.asarray(recs, EPISODE_DTYPE).tobytes(), group=group)
+    allr = np.concatenate([np.frombuffer(b, EPISODE_DTYPE) for b in parts])
+    return allr[np.lexsort((allr["env"], allr["step"]))]
