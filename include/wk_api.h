@@ -79,7 +79,8 @@ typedef struct wk_config {
   int GameSpeed;            /* 1 (UI only; ignored) */
   int Iterations;           /* 50 physics substeps per env-step */
   int MaxTimesteps;         /* 1000 */
-  int RoughFloor;           /* 0 (1 is rejected: SURVEY 8(f) next-3) */
+  int RoughFloor;           /* 0; 1: CreateRoughFloor's 10 static segments with a per-walker
+                               Philox terrain (1- and 16-lane mappings only) */
   int Epochs;               /* 5 */
   int BatchSize;            /* 64 */
   int UseGAE;               /* 0 */
@@ -217,7 +218,8 @@ int wk_step_traced(wk_ctx* ctx, const float* actions /* n_env*4 */, wk_pair_trac
 int wk_get_obs(wk_ctx* ctx, float* obs /* n_env*12 */);
 int wk_get_state(wk_ctx* ctx, float* state /* n_env*WK_STATE_FLOATS */);
 int wk_set_state(wk_ctx* ctx, const float* state /* n_env*WK_STATE_FLOATS */);
-int wk_get_body_view(wk_ctx* ctx, int env, int body /* 0..4 walker, 5 floor */, wk_body_view* out);
+int wk_get_body_view(wk_ctx* ctx, int env, int body /* 0..4 walker, 5 floor (5..14 rough-floor segments) */,
+                     wk_body_view* out);
 
 /* policy / value */
 int wk_get_weights(wk_ctx* ctx, float* params /* WK_NPARAM */);

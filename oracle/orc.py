@@ -50,6 +50,9 @@ def lib():
         sig = {
             "orc_hyper_defaults": (None, [C.POINTER(Hyper)]),
             "orc_env_create": (P, [C.POINTER(Hyper), F, I]),
+            "orc_env_create_floor": (P, [C.POINTER(Hyper), F, I, P]),
+            "orc_env_floor_body": (I, [P, I, P]),
+            "orc_terrain_draw": (I, [C.c_uint64, I, I]),
             "orc_env_destroy": (None, [P]),
             "orc_env_step": (None, [P, P, P, fp, C.POINTER(C.c_int), P]),
             "orc_env_get_obs": (None, [P, P]),
@@ -108,9 +111,16 @@ def hyper(**kw):
 class Env:
     """One reference Environment (walker + floor) with caller-supplied actions."""
 
-    def __init__(self, dx=0.0, material=0, **hkw):
+    def __init__(self, dx=0.0, material=0, rough=None, **hkw):
+        """rough: None = flat floor; else (seed, global env id) of the Philox terrain of
+        CreateRoughFloor (Environment.cs:230-261)"""
         self.h = hyper(**hkw)
-        self.p = lib().orc_env_create(C.byref(self.h), float(dx), int(material))
+        if rough is None:
+            self.p = lib().orc_env_create(C.byref(self.h), float(dx), int(material))
+        else:
+            self._draws = np.array(terrain_draws(*rough), np.int32)
+            self.p = lib().orc_env_create_floor(C.byref(self.h), float(dx), int(material),
+                                                _p(self._draws))
 
     def __del__(self):
         if getattr(self, "p", None):
@@ -140,6 +150,17 @@ class Env:
 
     def reset(self):
         lib().orc_env_reset(self.p)
+
+    def floor_bodies(self):
+        """vertices of the floor body / each rough-floor segment, list of (n, 2) arrays"""
+        out = []
+        buf = np.empty(12, np.float32)
+        for k in range(10):
+            nv = lib().orc_env_floor_body(self.p, k, _p(buf))
+            if nv == 0:
+                break
+            out.append(buf[:2 * nv].reshape(nv, 2).copy())
+        return out
 
     def joint_step(self, j):
         lib().orc_env_joint_step(self.p, int(j))
@@ -267,6 +288,11 @@ def synth_action(seed, env, t):
     a = np.empty(4, np.float32)
     lib().orc_synth_action(int(seed), int(env), int(t), _p(a))
     return a
+
+
+def terrain_draws(seed, env):
+    """the 11 Random.Next(0, 100) draws of CreateRoughFloor for one walker"""
+    return [lib().orc_terrain_draw(int(seed), int(env), i) for i in range(11)]
 
 
 def env_offset(seed, env):

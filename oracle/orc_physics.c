@@ -21,7 +21,8 @@
  *                                   CreateBodies :155-177, CreateJoints :180-188,
  *                                   AddAssociatedBodies :202-209, Reset :212-234)
  *   Environment.cs                 (Update :64-92, Step :96-122, StepObjects :126-143,
- *                                   CalculateReward :148-154, Reset :167-180, CreateFloor :211-226)
+ *                                   CalculateReward :148-154, Reset :167-180, CreateFloor :211-226,
+ *                                   CreateRoughFloor :230-261)
  */
 #include "wk_oracle.h"
 #include <float.h>
@@ -82,10 +83,13 @@ typedef struct {
 
 typedef struct { int a, b, ia, ib; float torque; } joint;
 
+enum { MAXB = 5 + ORC_ROUGH_SEGMENTS };
 struct orc_env {
   orc_hyper h;
-  body bodies[6];      /* indexed by ORC_LLL..ORC_FLOOR */
-  int order[6];        /* List<RigidBody> order */
+  body bodies[MAXB];   /* ORC_LLL..ORC_RLU, then the floor body / rough-floor segments */
+  int order[MAXB];     /* List<RigidBody> order */
+  int nbodies;         /* 6, or 15 with the rough floor */
+  int rough;
   joint joints[4];
   v2 position, prev_position;
   int terminal;
@@ -388,13 +392,13 @@ static int is_assoc(const body* b, int other) {
 
 static void resolve_collisions(orc_env* e, int self, orc_pair_trace* tr) {
   body* A = &e->bodies[self];
-  for (int k = 0; k < 6; k++) {
+  for (int k = 0; k < e->nbodies; k++) {
     int o = e->order[k];
     if (o == self) continue;
     if (is_assoc(A, o)) continue;
     body* B = &e->bodies[o];
     if (!aabb_overlap(A, B)) continue;
-    int pi = PAIR_IDX[self][o];
+    int pi = e->rough ? (o < ORC_FLOOR ? PAIR_IDX[self][o] : -1) : PAIR_IDX[self][o];
     if (tr && pi >= 0) tr->aabb_hit[pi] = 1;
     if (B->is_floor) A->collided = 1;
     if (A->is_floor) B->collided = 1;
@@ -464,7 +468,7 @@ void orc_env_step_objects(orc_env* e, float deltaTime, orc_pair_trace* trace) {
     if (tr) memset(tr, 0, sizeof(*tr));
     for (int j = 0; j < 4; j++)
       joint_step(e, &e->joints[j], tr ? &tr->joint_depth[j] : NULL, tr ? &tr->joint_impulse[j] : NULL);
-    for (int k = 0; k < 6; k++) body_step(e, e->order[k], deltaTime, tr);
+    for (int k = 0; k < e->nbodies; k++) body_step(e, e->order[k], deltaTime, tr);
   }
 }
 
@@ -532,9 +536,10 @@ void orc_env_reset(orc_env* e) {
   e->position = V(125.0f + e->dx, 800.0f);
   e->prev_position = e->position;
   create_creature(e);
-  e->order[0] = ORC_FLOOR;
-  e->order[1] = ORC_LLL; e->order[2] = ORC_LLU; e->order[3] = ORC_BODY;
-  e->order[4] = ORC_RLL; e->order[5] = ORC_RLU;
+  const int nf = e->nbodies - 5;  /* the floor body / segments keep their list positions */
+  for (int k = 0; k < nf; k++) e->order[k] = ORC_FLOOR + k;
+  e->order[nf + 0] = ORC_LLL; e->order[nf + 1] = ORC_LLU; e->order[nf + 2] = ORC_BODY;
+  e->order[nf + 3] = ORC_RLL; e->order[nf + 4] = ORC_RLU;
   e->post_reset = 1;
   initial_state(e);
 }
@@ -557,22 +562,55 @@ void orc_hyper_defaults(orc_hyper* h) {
   h->DeltaTime = (float)(166667.0 / 10000000.0);
 }
 
-orc_env* orc_env_create(const orc_hyper* h, float dx, int material) {
+/* CreateRoughFloor (Environment.cs:230-261), segments = 10, roughness = 100: draws[0] is
+ * the first previousVector's Random.Next(0, 100), draws[1..10] the segments' */
+static void create_rough_floor(orc_env* e, const int* draws) {
+  const int initialY = 800, initialX = -50, movement = 1200 / ORC_ROUGH_SEGMENTS;
+  v2 prev = V((float)initialX, (float)(initialY + draws[0]));
+  for (int i = 0; i < ORC_ROUGH_SEGMENTS; i++) {
+    int x = initialX + i * movement;
+    int y = 800 + draws[i + 1];
+    v2 pos[4] = {V((float)x, 1050.0f), prev, V((float)x, (float)y), V((float)(x + movement), 1050.0f)};
+    body_init(&e->bodies[ORC_FLOOR + i], ORC_MAT_METAL, pos, 4, 1, 1);
+    prev = V((float)x, (float)y);
+  }
+}
+
+orc_env* orc_env_create_floor(const orc_hyper* h, float dx, int material, const int* rough_draws) {
   orc_env* e = (orc_env*)calloc(1, sizeof(orc_env));
   e->h = *h;
   e->dx = dx;
   e->material = material;
-  /* Environment ctor (Environment.cs:39-51): walker first, then the floor */
+  e->rough = rough_draws != NULL;
+  e->nbodies = e->rough ? 5 + ORC_ROUGH_SEGMENTS : 6;
+  /* Environment ctor (Environment.cs:39-51): walker first, then the floor (CreateFloor :211-226) */
   e->position = V(125.0f + dx, 800.0f);
   e->prev_position = e->position;
   create_creature(e);
-  v2 fl[4] = {V(-50, 1050), V(-50, 900), V(1050, 900), V(1050, 1050)};
-  body_init(&e->bodies[ORC_FLOOR], ORC_MAT_METAL, fl, 4, 1, 1);
+  if (e->rough) {
+    create_rough_floor(e, rough_draws);
+  } else {
+    v2 fl[4] = {V(-50, 1050), V(-50, 900), V(1050, 900), V(1050, 1050)};
+    body_init(&e->bodies[ORC_FLOOR], ORC_MAT_METAL, fl, 4, 1, 1);
+  }
   e->order[0] = ORC_LLL; e->order[1] = ORC_LLU; e->order[2] = ORC_BODY;
-  e->order[3] = ORC_RLL; e->order[4] = ORC_RLU; e->order[5] = ORC_FLOOR;
+  e->order[3] = ORC_RLL; e->order[4] = ORC_RLU;
+  for (int k = 5; k < e->nbodies; k++) e->order[k] = k;
   e->post_reset = 0;
   initial_state(e);
   return e;
+}
+
+orc_env* orc_env_create(const orc_hyper* h, float dx, int material) {
+  return orc_env_create_floor(h, dx, material, NULL);
+}
+
+/* floor body k's vertices (x0, y0, x1, y1, ...); returns the vertex count */
+int orc_env_floor_body(const orc_env* e, int k, float* xy) {
+  if (k < 0 || k >= e->nbodies - 5) return 0;
+  const body* b = &e->bodies[ORC_FLOOR + k];
+  for (int i = 0; i < b->nv; i++) { xy[2 * i] = b->v[i].x; xy[2 * i + 1] = b->v[i].y; }
+  return b->nv;
 }
 
 void orc_env_destroy(orc_env* e) { free(e); }

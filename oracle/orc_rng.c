@@ -11,7 +11,7 @@
 #include "wk_oracle.h"
 #include <math.h>
 
-enum { ST_OFFSET = 1, ST_MAT = 2, ST_ACT = 3, ST_SYNTH = 4, ST_XAVIER = 5, ST_PERM = 6 };
+enum { ST_OFFSET = 1, ST_MAT = 2, ST_ACT = 3, ST_SYNTH = 4, ST_XAVIER = 5, ST_PERM = 6, ST_TERRAIN = 7 };
 
 static inline uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t* hi) {
   uint64_t p = (uint64_t)a * (uint64_t)b;
@@ -48,6 +48,16 @@ float orc_uniform_f(uint64_t key, uint32_t c0, uint32_t c1, uint32_t c2, uint32_
 
 float orc_env_offset(uint64_t seed, int env) {
   return 200.0f * orc_uniform_f(seed, (uint32_t)env, 0, 0, ST_OFFSET, 0);
+}
+
+/* Random.Next(0, roughness) (System.Random: (int)(Sample() * range) + min, in double) for
+ * CreateRoughFloor (Environment.cs:230-261): draw i = 0 is the first previousVector, draws
+ * 1..10 the segment heights.  Per-env Philox terrain replaces the unseeded Random (:242). */
+int orc_terrain_draw(uint64_t seed, int env, int i) {
+  uint32_t ctr[4] = {(uint32_t)env, (uint32_t)i, 0, ST_TERRAIN}, o[4];
+  orc_philox(seed, ctr, o);
+  double d = ((double)(o[0] >> 5) * 67108864.0 + (double)(o[1] >> 6)) * (1.0 / 9007199254740992.0);
+  return (int)(d * 100.0);
 }
 
 int orc_env_material(uint64_t seed, int env) {

@@ -37,7 +37,8 @@ enum {
   ORC_ST_POSTRESET = 109, /* 1 once the env has been reset (floor first in body list) */
   ORC_ST_TERMINAL = 110,  /* Walker.Terminal */
   ORC_ST_EPISODES = 111,  /* completed episodes */
-  ORC_STATE_FLOATS = 112
+  ORC_STATE_FLOATS = 112,
+  ORC_ROUGH_SEGMENTS = 10  /* CreateRoughFloor(segments = 10) */
 };
 
 /* candidate pair checks per substep, canonical index (this, other):
@@ -83,6 +84,11 @@ void orc_hyper_defaults(orc_hyper* h);
 /* ---------------- physics / environment ---------------- */
 typedef struct orc_env orc_env;
 orc_env* orc_env_create(const orc_hyper* h, float dx, int material);
+/* rough_draws: NULL = the flat floor; else the 11 Random.Next(0, 100) draws of
+ * CreateRoughFloor (Environment.cs:230-261), e.g. orc_terrain_draw(seed, env, 0..10) */
+orc_env* orc_env_create_floor(const orc_hyper* h, float dx, int material, const int* rough_draws);
+int orc_env_floor_body(const orc_env* e, int k, float* xy);
+int orc_terrain_draw(uint64_t seed, int env, int i);
 void orc_env_destroy(orc_env* e);
 /* one Environment.Update with a given (unclipped) action; clip as Environment.cs:78.
  * obs: 12 floats after the step (after auto-reset if done). trace: per-substep pair

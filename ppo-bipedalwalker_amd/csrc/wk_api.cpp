@@ -209,7 +209,8 @@ static int validate(const wk_config* c, std::string& why) {
   if (c->Lambda <= 0 || c->Lambda > 1) return bad("Invalid lambda value, should be in range 0<x<1");
   if (c->Epsilon <= 0 || c->Epsilon > 1) return bad("Invalid epsilon value, should be in range 0<x<1");
   if (c->LogStandardDeviation <= -5 || c->LogStandardDeviation >= 5) return bad("Invalid log standard deviation value, should be in range -5<x<5");
-  if (c->RoughFloor) return bad("RoughFloor is not supported by the batched kernel (SURVEY 8(f) next-3)");
+  if (c->RoughFloor && c->LanesPerWalker == 2)
+    return bad("RoughFloor runs on the 1- and 16-lane mappings (LanesPerWalker 0, 1 or 16)");
   if (c->CriticNeuralNetwork && strcmp(c->CriticNeuralNetwork, kCriticDefault) != 0) {
     snprintf(b, sizeof(b), "critic network '%s' unsupported: the kernels implement '%s'", c->CriticNeuralNetwork, kCriticDefault);
     why = b;
@@ -275,7 +276,8 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   P.env_offset = c.EnvOffset;
   // auto: the side-split pair mapping once it fills every SIMD twice (2 lanes x 32k
   // walkers = 1024 SIMDs x 2 waves), the 16-lane SAT rows below that
-  P.lanes = c.LanesPerWalker ? c.LanesPerWalker : (n_env >= 32768 ? 2 : 16);
+  P.lanes = c.LanesPerWalker ? c.LanesPerWalker : (c.RoughFloor || n_env < 32768 ? 16 : 2);
+  P.rough = c.RoughFloor ? 1 : 0;
   const float PI_F = 3.14159265358979323846f;
   x->lp_const = -logf(P.std_) - logf(sqrtf(2.0f * PI_F));
 
@@ -491,8 +493,25 @@ int wk_set_state(wk_ctx* c, const float* state) {
 }
 
 int wk_get_body_view(wk_ctx* c, int env, int body, wk_body_view* o) {
-  if (!c || !o || env < 0 || env >= c->n || body < 0 || body > 5) return WK_ERR_ARG;
+  if (!c || !o || env < 0 || env >= c->n || body < 0 || body >= (c->P.rough ? 15 : 6)) return WK_ERR_ARG;
   memset(o, 0, sizeof(*o));
+  if (c->P.rough && body >= 5) {  // rough-floor segment body - 5 (Environment.cs:230-261)
+    const int k = body - 5;
+    const uint32_t gid = (uint32_t)(c->cfg.EnvOffset + env);
+    const float x = -50.0f + 120.0f * (float)k;
+    const float yp = 800.0f + (float)wk::terrain_draw(c->seed, gid, k);
+    const float y = 800.0f + (float)wk::terrain_draw(c->seed, gid, k + 1);
+    const float v[4][2] = {{x, 1050.0f}, {k == 0 ? x : x - 120.0f, yp}, {x, y}, {x + 120.0f, 1050.0f}};
+    float sx = 0.0f, sy = 0.0f;
+    o->n_vertices = 4;
+    for (int i = 0; i < 4; i++) {
+      o->vertices[i][0] = v[i][0]; o->vertices[i][1] = v[i][1];
+      sx += v[i][0]; sy += v[i][1];
+    }
+    o->centroid[0] = sx * 0.25f; o->centroid[1] = sy * 0.25f;  // FindCentroid: sum * (1/4)
+    o->is_static = 1;
+    return WK_OK;
+  }
   if (body == 5) {  // the static Metal floor (Environment.cs:219-223)
     const float fl[4][2] = {{-50, 1050}, {-50, 900}, {1050, 900}, {1050, 1050}};
     o->n_vertices = 4;

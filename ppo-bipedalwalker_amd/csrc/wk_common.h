@@ -12,7 +12,7 @@
 
 namespace wk {
 
-enum Stream : uint32_t { ST_OFFSET = 1, ST_MAT = 2, ST_ACT = 3, ST_SYNTH = 4, ST_XAVIER = 5, ST_PERM = 6 };
+enum Stream : uint32_t { ST_OFFSET = 1, ST_MAT = 2, ST_ACT = 3, ST_SYNTH = 4, ST_XAVIER = 5, ST_PERM = 6, ST_TERRAIN = 7 };
 
 // canonical state layout (include/wk_api.h WK_STATE_FLOATS)
 enum : int {
@@ -67,6 +67,16 @@ WK_HD int env_material(uint64_t seed, uint32_t env) {
   int k = (int)(3.0f * u);
   if (k > 2) k = 2;
   return k == 0 ? 1 /*Ice*/ : (k == 1 ? 2 /*Rubber*/ : 0 /*Carpet*/);
+}
+
+// Random.Next(0, roughness = 100) of CreateRoughFloor (Environment.cs:230-261): System.Random
+// returns (int)(Sample() * range) + min with a double Sample().  Draw 0 is the first
+// previousVector's height, draws 1..10 the segments'; per-walker Philox terrain replaces
+// the unseeded Random (:242).
+WK_HD int terrain_draw(uint64_t seed, uint32_t env, int i) {
+  U4 o = philox(seed, env, (uint32_t)i, 0, ST_TERRAIN);
+  double d = ((double)(o.x >> 5) * 67108864.0 + (double)(o.y >> 6)) * (1.0 / 9007199254740992.0);
+  return (int)(d * 100.0);
 }
 
 WK_HD float synth_u(uint32_t w) { return (float)(w >> 8) * (1.0f / 16777216.0f); }
@@ -135,6 +145,7 @@ struct EnvParams {
   uint64_t seed;
   int env_offset;
   int lanes;            // lanes per walker in the env-step kernel (1, 2 or 16)
+  int rough;            // Hyperparameters.RoughFloor: 10 static floor segments
 };
 
 }  // namespace wk

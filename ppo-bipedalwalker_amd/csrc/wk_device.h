@@ -382,7 +382,7 @@ DEV V2 pick(const Poly<N>& p, int i) {
 // projection below MaxValue (index -1) the reference keeps Vector2.Zero and takes the
 // neighbours (index + 1) % N = 0 and Mod(index - 1, N) = N - 2.
 DEV uint32_t bsel(uint32_t m, float a, uint32_t b) { return (m & __float_as_uint(a)) | (~m & b); }
-template <int N>
+template <int N, bool SAFE = false>
 DEV void significant_face(const Poly<N>& P, V2 n, V2& fa, V2& fb, V2& fmax) {
   float mind = FLT_MAX;
   uint32_t sx = 0u, sy = 0u;
@@ -404,8 +404,9 @@ DEV void significant_face(const Poly<N>& P, V2 n, V2& fa, V2& fb, V2& fmax) {
   const V2 sig = mk(__uint_as_float(sx), __uint_as_float(sy));
   const V2 va = mk(__uint_as_float(ax), __uint_as_float(ay));
   const V2 vb = mk(__uint_as_float(bx), __uint_as_float(by));
-  V2 after = vnormalize_edge(vsub(sig, va));
-  V2 before = vnormalize_edge(vsub(sig, vb));
+  // SAFE: the polygon may have a zero edge, whose Normalize is NaN (and the compare false)
+  V2 after = SAFE ? vnormalize(vsub(sig, va)) : vnormalize_edge(vsub(sig, va));
+  V2 before = SAFE ? vnormalize(vsub(sig, vb)) : vnormalize_edge(vsub(sig, vb));
   const bool first = vdot(n, before) >= vdot(n, after);
   fa = first ? sig : va;
   fb = first ? vb : sig;
@@ -429,12 +430,12 @@ DEV int clip_vectors(V2 a, V2 b, V2 n, float offset, V2& o0, V2& o1) {
   return (int)ka + (int)kb + (int)kx;
 }
 
-template <int NA, int NB>
+template <int NA, int NB, bool SAFE = false>
 DEV int contact_points(const Poly<NA>& A, const Poly<NB>& B, V2 normal, V2& c0, V2& c1) {
   V2 ra, rb, rmax, ia, ib, imax;
   significant_face(A, normal, ra, rb, rmax);
   V2 rf = vsub(rb, ra);
-  significant_face(B, vneg(normal), ia, ib, imax);
+  significant_face<NB, SAFE>(B, vneg(normal), ia, ib, imax);
   V2 iv = vsub(ib, ia);
   if (fabsf(vdot(rf, normal)) > fabsf(vdot(iv, normal))) {  // selects, not a branch
     V2 t;
@@ -443,7 +444,7 @@ DEV int contact_points(const Poly<NA>& A, const Poly<NB>& B, V2 normal, V2& c0, 
     t = rmax; rmax = imax; imax = t;
     rf = vsub(rb, ra);
   }
-  rf = vnormalize_edge(rf);  // rb - ra is an edge of the reference face
+  rf = SAFE ? vnormalize(rf) : vnormalize_edge(rf);  // rb - ra: an edge of the reference face
   float offset = vdot(rf, ra);
   V2 p0 = mk(0.0f, 0.0f), p1 = mk(0.0f, 0.0f);
   const int k1 = clip_vectors(ia, ib, rf, offset, p0, p1);

@@ -207,15 +207,19 @@ DEV Poly<N> perturbed(const Poly<N>& p) {
 #endif
 
 // RigidBody.ResolveCollisions body for one (this=A, other=B) candidate
-// (Bodies/RigidBody.cs:66-96); B may be the static floor.
-template <int NA, int NB, bool BSTATIC, bool TRACE, int L>
+// (Bodies/RigidBody.cs:66-96); B may be the static floor.  GENERIC: B is a static floor
+// polygon other than the flat box (a rough-floor segment): its bounding box, SAT and
+// contact faces are evaluated in general, with Vector2.Normalize's NaN for a zero edge.
+template <int NA, int NB, bool BSTATIC, bool TRACE, int L, bool GENERIC = false>
 DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB,
                       bool& colA, PairTraceDev* tr, int pi, int sub, RegionProf* rp = nullptr) {
   static_assert(!BSTATIC || NB == 4, "the static body is the floor");
+  static_assert(!GENERIC || BSTATIC, "generic static floor polygon");
+  constexpr bool FLAT = BSTATIC && !GENERIC;
   float mnx, mny, mxx, mxy;  // A's bounding box (the floor pass of sat_floor reuses it)
   aabb(A, mnx, mny, mxx, mxy);
   bool ov;
-  if constexpr (BSTATIC) {
+  if constexpr (FLAT) {
     ov = mnx < 1050.0f && mxx > -50.0f && mny < 1050.0f && mxy > 900.0f;  // floor box
   } else {
     float b0x, b0y, b1x, b1y;
@@ -225,24 +229,24 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   rp_mark(rp, RP_AABB);
   DUP(1, { const auto Ap = perturbed(A); sink(aabb_overlap(Ap, B) ? 1.0f : 0.0f); });
   if (!ov) return;
-  if (TRACE && tr) tr->aabb_hit[pi] = 1;
+  if (TRACE && tr && pi >= 0) tr->aabb_hit[pi] = 1;
   if (BSTATIC) colA = true;  // body._isFloor -> Collided = true (:75)
   V2 n;
   float depth;
   bool hit;
   if constexpr (L > 1) hit = sat_row<L>(A, B, sub, n, depth);
-  else if constexpr (BSTATIC) hit = sat_floor(A, B, mnx, mny, mxx, mxy, n, depth);
+  else if constexpr (FLAT) hit = sat_floor(A, B, mnx, mny, mxx, mxy, n, depth);
   else hit = sat(A, B, n, depth);
   rp_mark(rp, RP_SAT);
   DUP(2, { const auto Ap = perturbed(A); V2 n2; float d2;
            const bool h2 = sat(Ap, B, n2, d2); sink(n2.x); sink(n2.y); sink(d2); sink(h2 ? 1.0f : 0.0f); });
   if (!hit) return;
   V2 c0, c1;
-  int nc = contact_points(A, B, n, c0, c1);
+  int nc = contact_points<NA, NB, GENERIC>(A, B, n, c0, c1);
   rp_mark(rp, RP_CONTACT);
   DUP(3, { const auto Ap = perturbed(A); V2 e0, e1;
            const int k2 = contact_points(Ap, B, n, e0, e1); sink(e0.x); sink(e1.y); sink((float)k2); });
-  if (TRACE && tr) {
+  if (TRACE && tr && pi >= 0) {
     tr->sat_hit[pi] = 1;
     tr->n_contacts[pi] = (uint8_t)nc;
     tr->normal[pi][0] = n.x;
@@ -269,7 +273,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   float j = calc_impulse(bA, bB, contact, 1.0f + e, n, rA, rB);
   V2 tangent = mk(-n.y, n.x);
   float jf = calc_impulse(bA, bB, contact, mu, tangent, rAF, rBF);
-  if (TRACE && tr) { tr->impulse[pi][0] = j; tr->impulse[pi][1] = jf; }
+  if (TRACE && tr && pi >= 0) { tr->impulse[pi][0] = j; tr->impulse[pi][1] = jf; }
   apply_impulses<BSTATIC>(bA, bB, n, j, rA, rB);
   apply_impulses<BSTATIC>(bA, bB, tangent, jf, rAF, rBF);
   rp_mark(rp, RP_IMPULSE);
@@ -313,15 +317,46 @@ DEV void integrate(Poly<N>& P, Dyn& D, float dt, float adx, float ady) {
   rotate(P, D.w * dt);
 }
 
-// one substep of Environment.StepObjects (:130-142)
-template <bool TRACE, int L>
-DEV void substep(EnvState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
-                 PairTraceDev* tr, int sub) {
-  Poly<4> fl;
-  floor_poly(fl);
+// Environment.CreateRoughFloor (Environment.cs:230-261), segment k of 10 (movement 120):
+// {(x, 1050), previousVector, (x, y), (x + 120, 1050)} with x = -50 + 120 k; the first
+// previousVector is (-50, 800 + draw 0), so segment 0 has three vertices on x = -50 (and
+// a zero edge when draws 0 and 1 are equal).  All coordinates are small integers (exact).
+DEV void rough_segment(Poly<4>& f, int k, float yprev, float y) {
+  const float x = -50.0f + 120.0f * (float)k;
+  f.x[0] = x;                         f.y[0] = 1050.0f;
+  f.x[1] = k == 0 ? x : x - 120.0f;   f.y[1] = yprev;
+  f.x[2] = x;                         f.y[2] = y;
+  f.x[3] = x + 120.0f;                f.y[3] = 1050.0f;
+  find_centroid(f);
+}
+
+// a walker part's candidate pair(s) against the floor: the flat box (Environment.cs:211-226)
+// or, with RoughFloor, the 10 static segments in list order (ter: this walker's 11 terrain
+// heights in LDS, stride 64)
+template <int N, bool TRACE, int L, bool ROUGH>
+DEV void floor_pairs(Poly<N>& P, Dyn& D, const Mat& m, bool& col, PairTraceDev* tr, int pi,
+                     int sub, const float* ter) {
   Dyn dfl;
   zero_dyn(dfl);
   const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};  // Metal, static: inverse mass/inertia 0
+  if constexpr (ROUGH) {
+#pragma unroll 1
+    for (int k = 0; k < 10; k++) {
+      Poly<4> seg;
+      rough_segment(seg, k, ter[k * 64], ter[(k + 1) * 64]);
+      resolve_pair<N, 4, true, TRACE, L, true>(P, D, m, seg, dfl, mf, col, tr, -1, sub);
+    }
+  } else {
+    Poly<4> fl;
+    floor_poly(fl);
+    resolve_pair<N, 4, true, TRACE, L>(P, D, m, fl, dfl, mf, col, tr, pi, sub);
+  }
+}
+
+// one substep of Environment.StepObjects (:130-142)
+template <bool TRACE, int L, bool ROUGH>
+DEV void substep(EnvState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
+                 PairTraceDev* tr, int sub, const float* ter) {
   // joints: [bodyJointLeft, bodyJointRight, leftJoint, rightJoint] (Walker.cs:182-187)
   joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.llu, s.dllu, mp, tr, 0);
   joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.rlu, s.drlu, mp, tr, 1);
@@ -329,31 +364,31 @@ DEV void substep(EnvState& s, const Mat& mp, const Mat& mb, float dt, float adx,
   joint_step<6, 6, 2, 3, TRACE>(s.rlu, s.drlu, mp, s.rll, s.drll, mp, tr, 3);
   // bodies in list order; the floor's own step is a no-op (static, zero velocity).
   // Episode 0 lists the floor last, every later episode first (Walker.cs:212-234):
-  // that only changes the order of each leg segment's two candidate pairs.
+  // that only changes the order of each leg segment's candidate pairs.
   integrate(s.lll, s.dlll, dt, adx, ady);
 #pragma unroll 1
   for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, L>(s.lll, s.dlll, mp, fl, dfl, mf, s.clll, tr, 1, sub);
+    if ((q == 0) == s.post) floor_pairs<6, TRACE, L, ROUGH>(s.lll, s.dlll, mp, s.clll, tr, 1, sub, ter);
     else resolve_pair<6, 6, false, TRACE, L>(s.lll, s.dlll, mp, s.llu, s.dllu, mp, s.clll, tr, 0, sub);
   }
   integrate(s.llu, s.dllu, dt, adx, ady);
 #pragma unroll 1
   for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, L>(s.llu, s.dllu, mp, fl, dfl, mf, s.cllu, tr, 3, sub);
+    if ((q == 0) == s.post) floor_pairs<6, TRACE, L, ROUGH>(s.llu, s.dllu, mp, s.cllu, tr, 3, sub, ter);
     else resolve_pair<6, 6, false, TRACE, L>(s.llu, s.dllu, mp, s.lll, s.dlll, mp, s.cllu, tr, 2, sub);
   }
   integrate(s.body, s.dbody, dt, adx, ady);
-  resolve_pair<5, 4, true, TRACE, L>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody, tr, 4, sub);
+  floor_pairs<5, TRACE, L, ROUGH>(s.body, s.dbody, mb, s.cbody, tr, 4, sub, ter);
   integrate(s.rll, s.drll, dt, adx, ady);
 #pragma unroll 1
   for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, L>(s.rll, s.drll, mp, fl, dfl, mf, s.crll, tr, 6, sub);
+    if ((q == 0) == s.post) floor_pairs<6, TRACE, L, ROUGH>(s.rll, s.drll, mp, s.crll, tr, 6, sub, ter);
     else resolve_pair<6, 6, false, TRACE, L>(s.rll, s.drll, mp, s.rlu, s.drlu, mp, s.crll, tr, 5, sub);
   }
   integrate(s.rlu, s.drlu, dt, adx, ady);
 #pragma unroll 1
   for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, L>(s.rlu, s.drlu, mp, fl, dfl, mf, s.crlu, tr, 8, sub);
+    if ((q == 0) == s.post) floor_pairs<6, TRACE, L, ROUGH>(s.rlu, s.drlu, mp, s.crlu, tr, 8, sub, ter);
     else resolve_pair<6, 6, false, TRACE, L>(s.rlu, s.drlu, mp, s.rll, s.drll, mp, s.crlu, tr, 7, sub);
   }
 }
@@ -508,7 +543,7 @@ DEV bool state_finite(const EnvState& s) {
 // L lanes per walker (a "row"): the Gauss-Seidel chain runs replicated in every lane of
 // the row (bit-identical state), SAT axes are split one per lane (sat_row); lane 0 of
 // the row owns all stores.  L = 1 is the plain one-walker-per-lane mapping.
-template <bool POLICY, bool RECORD, bool TRACE, int L>
+template <bool POLICY, bool RECORD, bool TRACE, int L, bool ROUGH>
 __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArgs A) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = tid / L, sub = tid % L;
@@ -516,6 +551,15 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArg
   if (e >= n) return;  // whole rows exit together
   const bool leader = sub == 0;
   __shared__ float pol_lds[(L == 16 && POLICY) ? 4 * 192 : 1];
+  // the walker's rough-floor heights 800 + Random.Next(0, 100), [draw][walker of block]:
+  // each lane writes and later reads only its own walker's column (no barrier needed)
+  __shared__ float ter_lds[ROUGH ? 11 * 64 : 1];
+  float* ter = ter_lds + (threadIdx.x / L);
+  if constexpr (ROUGH) {
+#pragma unroll 1
+    for (int i = 0; i < 11; i++)
+      ter[i * 64] = 800.0f + (float)terrain_draw(P.seed, (uint32_t)(P.env_offset + e), i);
+  }
   EnvState s;
   load_state(s, A.st, e, n);
   const float dx = A.dxoff[e];
@@ -582,7 +626,7 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArg
         PairTraceDev z = {};
         *tr = z;
       }
-      substep<TRACE, L>(s, mp, mb, dt, adx, ady, tr, sub);
+      substep<TRACE, L, ROUGH>(s, mp, mb, dt, adx, ady, tr, sub, ter);
     }
     // Walker.Update
     s.prevx = s.posx; s.prevy = s.posy;
@@ -1136,15 +1180,20 @@ __global__ void k_returns(int n, int T, int use_gae, float gamma, float lambda,
 
 // host-side launch shims (C++ linkage, used by wk_api.cpp)
 namespace wk {
-template <int L>
-static void launch_lanes(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
+template <int L, bool ROUGH>
+static void launch_lanes_floor(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
   dim3 blk(64), grd((unsigned)(((size_t)P.n_env * L + 63) / 64));
   switch (mode) {
-    case 0: hipLaunchKernelGGL((k_env_step<false, false, false, L>), grd, blk, 0, s, P, A); break;
-    case 1: hipLaunchKernelGGL((k_env_step<false, false, true, L>), grd, blk, 0, s, P, A); break;
-    case 2: hipLaunchKernelGGL((k_env_step<true, false, false, L>), grd, blk, 0, s, P, A); break;
-    default: hipLaunchKernelGGL((k_env_step<true, true, false, L>), grd, blk, 0, s, P, A); break;
+    case 0: hipLaunchKernelGGL((k_env_step<false, false, false, L, ROUGH>), grd, blk, 0, s, P, A); break;
+    case 1: hipLaunchKernelGGL((k_env_step<false, false, true, L, ROUGH>), grd, blk, 0, s, P, A); break;
+    case 2: hipLaunchKernelGGL((k_env_step<true, false, false, L, ROUGH>), grd, blk, 0, s, P, A); break;
+    default: hipLaunchKernelGGL((k_env_step<true, true, false, L, ROUGH>), grd, blk, 0, s, P, A); break;
   }
+}
+template <int L>
+static void launch_lanes(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
+  if (P.rough) launch_lanes_floor<L, true>(mode, P, A, s);
+  else launch_lanes_floor<L, false>(mode, P, A, s);
 }
 static void launch_side(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
   dim3 blk(SIDE_BLOCK), grd((unsigned)(((size_t)P.n_env * 2 + SIDE_BLOCK - 1) / SIDE_BLOCK));

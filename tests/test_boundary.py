@@ -51,7 +51,7 @@ def test_struct_layouts(wk):
     ("Gamma", 1.5, "gamma"),
     ("Epsilon", 0.0, "epsilon"),
     ("LogStandardDeviation", 5.0, "log standard deviation"),
-    ("RoughFloor", 1, "RoughFloor"),
+    ("GameSpeed", 10, "game speed"),
     ("ActorNeuralNetwork", "Input |32| (ReLU) |4| Output", "actor network"),
 ])
 def test_invalid_config_rejected_without_gpu(wk, field, value, msg):
@@ -84,3 +84,13 @@ def test_bad_arguments(wk):
     assert lib.wk_create(None, 0, 0, 1, C.byref(h)) == -1
     assert lib.wk_destroy(None) == 0
     assert lib.wk_step(None, None, 1, None, None, None, None) == -1
+
+
+def test_rough_floor_needs_row_mappings(wk):
+    """RoughFloor runs on the 1- and 16-lane mappings; the 2-lane leg split is refused
+    (before any device is touched)"""
+    lib = wk.load_library()
+    cfg = wk.default_config(RoughFloor=1, LanesPerWalker=2)
+    h = C.c_void_p()
+    assert lib.wk_create(C.byref(cfg), 0, 4, 1, C.byref(h)) == -3
+    assert b"RoughFloor" in lib.wk_last_error(None)
