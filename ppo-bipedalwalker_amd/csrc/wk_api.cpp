@@ -62,7 +62,7 @@ struct wk_ctx {
   double* ep_acc = nullptr;       // [n] running episode reward
   int32_t* ep_len = nullptr;      // [n]
   void* ep_scratch = nullptr;     // [T][n] float2
-  uint32_t* ep_rowcnt = nullptr;  // [T]
+  uint32_t* ep_rowcnt = nullptr;  // [T][tiles] episode counts per (row, 4,096-walker tile)
   uint64_t* ep_count = nullptr;   // device: records appended since the last drain
   wk::EpisodeRecDev* ep_log = nullptr;
   uint64_t ep_cap = 0;
@@ -309,7 +309,7 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   ALLOC(x->ep_acc, sizeof(double) * n);
   ALLOC(x->ep_len, sizeof(int32_t) * n);
   ALLOC(x->ep_scratch, sizeof(float) * 2 * n * T);
-  ALLOC(x->ep_rowcnt, sizeof(uint32_t) * T);
+  ALLOC(x->ep_rowcnt, sizeof(uint32_t) * wk::episode_count_cells((int)n, T));
   ALLOC(x->ep_count, sizeof(uint64_t));
   ALLOC(x->ep_log, sizeof(wk::EpisodeRecDev) * x->ep_cap);
   ALLOC(x->loss_log, sizeof(float) * 2 * x->loss_cap);
@@ -330,7 +330,7 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
       hipMemset(x->td, 0, n * T) != hipSuccess ||
       hipMemset(x->ep_acc, 0, sizeof(double) * n) != hipSuccess ||
       hipMemset(x->ep_len, 0, sizeof(int32_t) * n) != hipSuccess ||
-      hipMemset(x->ep_rowcnt, 0, sizeof(uint32_t) * T) != hipSuccess ||
+      hipMemset(x->ep_rowcnt, 0, sizeof(uint32_t) * wk::episode_count_cells((int)n, T)) != hipSuccess ||
       hipMemset(x->ep_count, 0, sizeof(uint64_t)) != hipSuccess) {
     x->err = "initial upload failed";
     return fail(WK_ERR_HIP);

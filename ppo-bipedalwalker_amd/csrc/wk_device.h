@@ -7,6 +7,7 @@
 #pragma once
 #include <float.h>
 #include "wk_common.h"
+#include "wk_sincos_small.h"
 
 namespace wk {
 
@@ -137,10 +138,14 @@ DEV void move(Poly<N>& p, V2 d) {
 
 // Skeleton.Rotate (Skeleton.cs:89-97): XNA CreateRotationZ uses (float)Math.Cos/Sin of
 // the double-promoted angle; Vector2.Transform(p, M) = (p.x*M11 + p.y*M21 + M41, ...)
+// |angle| <= 0.25 (every substep rotation in practice: w * dt with dt = 1/3000 s) takes
+// the short Taylor form, proven equal after the (float) rounding to the C library's
+// sin / cos for every float in range (tests/cpp/sincos_small_check.c, exhaustive).
 template <int N>
 DEV void rotate(Poly<N>& p, float angle) {
   double sd, cd;
-  sincos((double)angle, &sd, &cd);
+  if (__builtin_fabsf(angle) <= 0.25f) wk_sincos_small((double)angle, &sd, &cd);
+  else sincos((double)angle, &sd, &cd);
   const float c = (float)cd, s = (float)sd;
   const float m11 = c, m12 = s, m21 = -s, m22 = c;
 #pragma unroll
@@ -206,7 +211,12 @@ DEV void project2(float ax, float ay, const Poly<NA>& A, const Poly<NB>& B, floa
 // (Packed v_pk_mul/v_pk_add projections, two axes per instruction, measured 1.7x slower
 // on gfx950: each packed result needs a wait state before use and the pair costs two
 // passes anyway.  Scalar ops it is.)
-template <int NP, int NQ>
+// FLOORQ: Q is the flat floor box {x in (-50, 1050)} x {y in (900, 1050)}, all four
+// corner combinations.  Round-to-nearest addition is monotonic in each operand, so
+// min over corners of fl(fl(ax x) + fl(ay y)) = fl(min_x fl(ax x) + min_y fl(ay y)) (and
+// likewise max): the box projects in 4 products, 2 min, 2 max, 2 adds instead of a
+// 4-vertex loop -- the same values (a zero's sign aside, which no overlapping axis sees).
+template <int NP, int NQ, bool FLOORQ = false>
 DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, float& depth) {
 #pragma unroll
   for (int i = 0; i < NP; i++) {
@@ -216,7 +226,21 @@ DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, 
     const bool valid = !(axis.x == 0.0f && axis.y == 0.0f);
     axis = vnormalize_edge(axis);  // garbage for a zero edge: masked by `valid`
     float pmin, pmax, qmin, qmax;
-    project2(axis.x, axis.y, P, Q, pmin, pmax, qmin, qmax);
+    if constexpr (FLOORQ) {
+      pmin = FLT_MAX; pmax = -FLT_MAX;
+#pragma unroll
+      for (int k = 0; k < NP; k++) {
+        const float p = axis.x * P.x[k] + axis.y * P.y[k];
+        pmin = __builtin_fminf(pmin, p);
+        pmax = __builtin_fmaxf(pmax, p);
+      }
+      const float x0 = axis.x * -50.0f, x1 = axis.x * 1050.0f;
+      const float y0 = axis.y * 900.0f, y1 = axis.y * 1050.0f;
+      qmin = __builtin_fminf(x0, x1) + __builtin_fminf(y0, y1);
+      qmax = __builtin_fmaxf(x0, x1) + __builtin_fmaxf(y0, y1);
+    } else {
+      project2(axis.x, axis.y, P, Q, pmin, pmax, qmin, qmax);
+    }
     const float temp = __builtin_fminf(qmax - pmin, pmax - qmin);
     const bool overlapping = (pmin < qmax) && (qmin < pmax);
     sep = sep || (valid && !overlapping);
@@ -249,7 +273,7 @@ DEV bool sat_floor(const Poly<NA>& A, const Poly<4>& F, float mnx, float mny, fl
   normal = mk(0.0f, 0.0f);
   depth = FLT_MAX;
   bool sep = false;
-  axis_pass(A, F, sep, normal, depth);
+  axis_pass<NA, 4, true>(A, F, sep, normal, depth);
   floor_axis(-50.0f, 1050.0f, mnx, mxx, 1.0f, 0.0f, sep, normal, depth);
   floor_axis(900.0f, 1050.0f, mny, mxy, -0.0f, 1.0f, sep, normal, depth);
   floor_axis(-1050.0f, 50.0f, -mxx, -mnx, -1.0f, 0.0f, sep, normal, depth);

@@ -111,12 +111,13 @@ struct EpisodeArgs {
   double* acc;               // [n] running episode reward (carried across rollouts)
   int32_t* len;              // [n] running episode length
   float2* scratch;           // [T][n] (total, length bits), written where done
-  uint32_t* row_cnt;         // [T], zero on entry and exit
+  uint32_t* row_cnt;         // [episode_count_cells(n, T)], zero on entry and exit
   uint64_t* log_count;       // records appended so far (may exceed cap: dropped)
   uint64_t cap;
   EpisodeRecDev* log;
 };
 hipError_t launch_episode_log(const EpisodeArgs& a, hipStream_t s);
+int episode_count_cells(int n, int T);
 hipError_t launch_episode_reset(int n, const uint8_t* mask, double* acc, int32_t* len,
                                 hipStream_t s);
 

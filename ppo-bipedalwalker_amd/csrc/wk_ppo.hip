@@ -324,6 +324,37 @@ __global__ void k_grad_reduce2_adam(const float* __restrict__ part2, int ngroups
   if (p < NPARAM) adam_param(a, p, acc);
 }
 
+// One-launch form of the two stages for nblocks <= RG * RG, bit-identical association
+// (RG consecutive slabs in order, then the groups in order): a block owns 16 parameters;
+// thread (group gi, parameter pi) folds its group's RG slabs, and the 16 group sums are
+// folded in order through LDS.  ADAM: the single-GPU tail applies Adam as well.
+template <bool ADAM>
+__global__ __launch_bounds__(256) void k_grad_reduce_fused(const float* __restrict__ partial,
+                                                           int nblocks, float* grad, AdamArgs a) {
+  __shared__ float gs[RG][17];
+  const int pi = threadIdx.x & 15, gi = threadIdx.x >> 4;
+  const int p = blockIdx.x * 16 + pi;
+  const int ngroups = (nblocks + RG - 1) / RG;
+  float acc = 0.0f;
+  if (p < SLAB && gi < ngroups) {
+    const int b0 = gi * RG;
+    float v[RG];
+#pragma unroll
+    for (int j = 0; j < RG; j++) v[j] = (b0 + j < nblocks) ? partial[(size_t)(b0 + j) * SLAB + p] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < RG; j++)
+      if (b0 + j < nblocks) acc = acc + v[j];
+  }
+  gs[gi][pi] = acc;
+  __syncthreads();
+  if (gi == 0 && p < SLAB) {
+    float t = 0.0f;
+    for (int g = 0; g < ngroups; g++) t = t + gs[g][pi];
+    grad[p] = t;
+    if (ADAM && p < NPARAM) adam_param(a, p, t);
+  }
+}
+
 // Normalize (PPOAgent.cs:461-472): LINQ Average/Sum accumulate in double
 __global__ void k_normalize(float* x, int n, float eps_clip) {
   __shared__ double red[1024];
@@ -402,6 +433,11 @@ hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t 
 }
 hipError_t launch_grad_reduce(const float* partial, int nblocks, float* part2, float* grad,
                               hipStream_t s) {
+  if (nblocks <= RG * RG) {
+    hipLaunchKernelGGL(k_grad_reduce_fused<false>, dim3((SLAB + 15) / 16), dim3(256), 0, s,
+                       partial, nblocks, grad, AdamArgs{});
+    return hipGetLastError();
+  }
   const int ng = (nblocks + RG - 1) / RG;
   hipLaunchKernelGGL(k_grad_reduce1, dim3((SLAB + 255) / 256, ng), dim3(256), 0, s, partial,
                      nblocks, part2);
@@ -411,6 +447,11 @@ hipError_t launch_grad_reduce(const float* partial, int nblocks, float* part2, f
 int grad_reduce_groups(int nblocks) { return (nblocks + RG - 1) / RG; }
 hipError_t launch_grad_reduce_adam(const float* partial, int nblocks, float* part2, float* grad,
                                    const AdamArgs& a, hipStream_t s) {
+  if (nblocks <= RG * RG) {
+    hipLaunchKernelGGL(k_grad_reduce_fused<true>, dim3((SLAB + 15) / 16), dim3(256), 0, s,
+                       partial, nblocks, grad, a);
+    return hipGetLastError();
+  }
   const int ng = (nblocks + RG - 1) / RG;
   hipLaunchKernelGGL(k_grad_reduce1, dim3((SLAB + 255) / 256, ng), dim3(256), 0, s, partial,
                      nblocks, part2);
