@@ -176,7 +176,9 @@ def main():
         "rollout_env_steps_per_s": world * shard.n_local * args.horizon * args.steps / (phys_ms_max * 1e-3),
         "roofline": {
             "bound": "mfma",
-            "kernel": "k_env_step<policy,record> (fused rollout: physics + policy)",
+            "kernel": {2: "k_env_side<true,true,false>", 16: "k_env_step<true,true,false,16>",
+                       1: "k_env_step<true,true,false,1>"}[args.lanes or (2 if shard.n_local >= 32768 else 16)]
+                      + " (fused rollout: physics + policy)",
             "achieved": achieved_tflops,
             "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s",
