@@ -74,8 +74,48 @@ void k_ppo_grad_mfma(GradArgs ga) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, g = lane >> 4;
 
-  // ---- stage the weight image (already in operand order, wk_mfma_layout.h) ----
-  for (int e = tid; e < WEND / 4; e += 64 * WAVES) ((f4*)lds)[e] = ((const f4*)ga.Wz)[e];
+#ifdef WK_GRAD_NOLOOP  // probe: the launch without its chunk loop (fixed-cost measurement)
+  const int nchunks = 0;
+#else
+  const int nchunks = (ga.samples + 15) / 16;
+#endif
+  const int nw = gridDim.x * WAVES;
+  // gather (CreateBatches, PPOAgent.cs:512-533), one chunk ahead of the math
+  struct Smp { f4 sv; float act, lpo, ret, adv; };
+  auto gather = [&](int c) {
+    Smp m;
+    const int pos = c * 16 + n;
+    uint32_t idx = ga.base + (uint32_t)(pos < ga.samples ? pos : 0);
+    if (ga.use_perm) idx = perm_apply(idx, ga.pk);
+    m.sv = f4{1.0f, 0.0f, 0.0f, 0.0f};  // lane group 3: the bias column
+    if (g < 3) m.sv = *(const f4*)(ga.states + (size_t)idx * 12 + 4 * g);
+    m.act = ga.actions[(size_t)idx * 4 + g];
+    m.lpo = ga.logp_old[(size_t)idx * 4 + g];
+    m.ret = ga.returns[idx];
+    m.adv = ga.adv[idx];
+    return m;
+  };
+  int c = blockIdx.x * WAVES + wave;
+  // the first chunk's gather is in flight while the weights are staged
+  Smp nxt = gather(c < nchunks ? c : 0);
+
+  // ---- stage the weight image (already in operand order, wk_mfma_layout.h): every
+  // thread's loads are issued before its first LDS write, so the copy costs one L2
+  // round trip instead of one per 4 KB ----
+  {
+    constexpr int NV = WEND / 4, PER = (NV + 64 * WAVES - 1) / (64 * WAVES);
+    f4 wv[PER];
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+      const int e = tid + i * 64 * WAVES;
+      if (e < NV) wv[i] = ((const f4*)ga.Wz)[e];
+    }
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+      const int e = tid + i * 64 * WAVES;
+      if (e < NV) ((f4*)lds)[e] = wv[i];
+    }
+  }
   float* cb = lds + WEND + wave * CHUNK;
   for (int e = lane; e < 256; e += 64) cb[C_G3 + e] = 0.0f;
   __syncthreads();
@@ -115,29 +155,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
 #pragma unroll
     for (int d = 0; d < 4; d++) w3[d][Mt] = *(const f4*)(lds + W3 + d * 64 + 16 * Mt + 4 * g);
   }
-#ifdef WK_GRAD_NOLOOP  // probe: the launch without its chunk loop (fixed-cost measurement)
-  const int nchunks = 0;
-#else
-  const int nchunks = (ga.samples + 15) / 16;
-#endif
-  const int nw = gridDim.x * WAVES;
-  // gather (CreateBatches, PPOAgent.cs:512-533), one chunk ahead of the math
-  struct Smp { f4 sv; float act, lpo, ret, adv; };
-  auto gather = [&](int c) {
-    Smp m;
-    const int pos = c * 16 + n;
-    uint32_t idx = ga.base + (uint32_t)(pos < ga.samples ? pos : 0);
-    if (ga.use_perm) idx = perm_apply(idx, ga.pk);
-    m.sv = f4{1.0f, 0.0f, 0.0f, 0.0f};  // lane group 3: the bias column
-    if (g < 3) m.sv = *(const f4*)(ga.states + (size_t)idx * 12 + 4 * g);
-    m.act = ga.actions[(size_t)idx * 4 + g];
-    m.lpo = ga.logp_old[(size_t)idx * 4 + g];
-    m.ret = ga.returns[idx];
-    m.adv = ga.adv[idx];
-    return m;
-  };
-  int c = blockIdx.x * WAVES + wave;
-  Smp nxt = gather(c < nchunks ? c : 0);
 #pragma unroll 1
   for (; c < nchunks; c += nw) {
     const Smp cur = nxt;
