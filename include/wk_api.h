@@ -160,6 +160,37 @@ typedef struct wk_body_view {
   int is_static;
 } wk_body_view;
 
+/* Scene prop (extension of SURVEY 8(f) next-3): a Square / Triangle / Hexagon body built by
+ * <Shape>.FromSize(material, (cx, cy), size, isStatic) (Objects/RigidBodies/Square.cs:18-31,
+ * Triangle.cs:18-30, Hexagon.cs:18-33), then SmoothCorners(smooth) (Skeleton.cs:33-53; the
+ * centroid keeps its FromSize value), SetLinearVelocity((vx, vy)), SetAngularVelocity(w) and
+ * AddAcceleration((ax, ay)) (RigidBody.cs:143-183; gravity would be (0, 980)).  Every walker
+ * gets its own copy, listed after the floor: the line a maintainer adds after CreateFloor()
+ * in the Environment constructor (Environment.cs:39-51).  Walker resets keep the props. */
+enum { WK_SHAPE_SQUARE = 0, WK_SHAPE_TRIANGLE = 1, WK_SHAPE_HEXAGON = 2 };
+enum { WK_MAX_PROPS = 4, WK_PROP_MAXV = 24, WK_SCENE_MAX_VERTS = 32 };
+typedef struct wk_prop {
+  int32_t shape;      /* WK_SHAPE_* */
+  int32_t smooth;     /* SmoothCorners count: vertices = 4 / 3 / 6 times 2^smooth, <= 24 */
+  int32_t material;   /* 0 Carpet, 1 Ice, 2 Rubber, 3 Metal, 4 Wood, 5 Paper, 6 Titanium,
+                         7 SuperRubber (Materials/<Name>.cs) */
+  int32_t is_static;
+  float cx, cy, size;
+  float vx, vy, w;    /* initial linear / angular velocity */
+  float ax, ay;       /* acceleration */
+} wk_prop;
+
+/* one scene prop of one env (Renderer.RenderRigidObject) */
+typedef struct wk_prop_view {
+  int n_vertices;
+  float vertices[WK_PROP_MAXV][2];
+  float centroid[2];
+  float linear_velocity[2];
+  float angular_velocity;
+  float angle;
+  int is_static;
+} wk_prop_view;
+
 typedef struct wk_ppo_args {
   int epochs;          /* 0 -> config Epochs */
   int minibatch;       /* 0 -> config Minibatch */
@@ -222,6 +253,11 @@ int wk_get_body_view(wk_ctx* ctx, int env, int body /* 0..4 walker, 5 floor (5..
                      wk_body_view* out);
 
 /* policy / value */
+/* Scene props for every walker (n_props <= WK_MAX_PROPS, at most WK_SCENE_MAX_VERTS vertices
+ * in total; 0 removes them), each initialised as described at wk_prop.  With props the
+ * env-step runs the one-lane scene kernel (LanesPerWalker 0 or 1; not with RoughFloor). */
+int wk_set_scene(wk_ctx* ctx, const wk_prop* props, int n_props);
+int wk_get_prop_view(wk_ctx* ctx, int env, int prop, wk_prop_view* out);
 int wk_get_weights(wk_ctx* ctx, float* params /* WK_NPARAM */);
 int wk_set_weights(wk_ctx* ctx, const float* params);
 int wk_get_adam(wk_ctx* ctx, float* m, float* v, int* t);
@@ -260,7 +296,8 @@ int wk_parse_weights(const char* critic_text, const char* actor_text, float* par
 
 /* Binary checkpoint for bit-exact resume (new; the reference persists only weights):
  * weights, Adam m / v / t, every walker record, Philox step counters, start offsets,
- * materials, running episode rewards / lengths and the episode-log clock (the episode and
+ * materials, running episode rewards / lengths, the episode-log clock and the scene props
+ * (descriptions and every walker's prop state; loading replaces the context's scene) (the episode and
  * loss logs are not included: drain them first).  Loading requires the same n_env, seed and EnvOffset; it invalidates the
  * trajectory buffer (roll out again before wk_ppo_update). */
 int wk_checkpoint_save(wk_ctx* ctx, const char* path);

@@ -14,7 +14,32 @@ LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
 
 STATE_FLOATS = 112
 NPARAM = 6149
-MAT = {"Carpet": 0, "Ice": 1, "Rubber": 2, "Metal": 3}
+MAT = {"Carpet": 0, "Ice": 1, "Rubber": 2, "Metal": 3, "Wood": 4, "Paper": 5, "Titanium": 6,
+       "SuperRubber": 7}
+SHAPE = {"Square": 0, "Triangle": 1, "Hexagon": 2}
+PROP_MAXV = 24
+
+
+class Prop(C.Structure):
+    """scene prop (same layout as wk_prop, include/wk_api.h)"""
+    _fields_ = [("shape", C.c_int32), ("smooth", C.c_int32), ("material", C.c_int32),
+                ("is_static", C.c_int32), ("cx", C.c_float), ("cy", C.c_float),
+                ("size", C.c_float), ("vx", C.c_float), ("vy", C.c_float), ("w", C.c_float),
+                ("ax", C.c_float), ("ay", C.c_float)]
+
+
+def make_prop(shape="Square", smooth=0, material="Wood", is_static=False, cx=0.0, cy=0.0,
+              size=40.0, vx=0.0, vy=0.0, w=0.0, ax=0.0, ay=0.0):
+    return Prop(SHAPE.get(shape, shape), int(smooth), MAT.get(material, material),
+                int(bool(is_static)), cx, cy, size, vx, vy, w, ax, ay)
+
+
+def prop_vertices(p):
+    buf = np.empty(2 * PROP_MAXV, np.float32)
+    n = lib().orc_prop_vertices(C.byref(p), _p(buf))
+    if n < 0:
+        raise ValueError("bad prop")
+    return buf[:2 * n].reshape(n, 2).copy()
 
 
 class Hyper(C.Structure):
@@ -54,6 +79,9 @@ def lib():
             "orc_env_floor_body": (I, [P, I, P]),
             "orc_terrain_draw": (I, [C.c_uint64, I, I]),
             "orc_env_destroy": (None, [P]),
+            "orc_prop_vertices": (I, [P, P]),
+            "orc_env_add_prop": (I, [P, P]),
+            "orc_env_prop": (I, [P, I, P, P]),
             "orc_env_step": (None, [P, P, P, fp, C.POINTER(C.c_int), P]),
             "orc_env_get_obs": (None, [P, P]),
             "orc_env_dump": (None, [P, P]),
@@ -111,9 +139,10 @@ def hyper(**kw):
 class Env:
     """One reference Environment (walker + floor) with caller-supplied actions."""
 
-    def __init__(self, dx=0.0, material=0, rough=None, **hkw):
+    def __init__(self, dx=0.0, material=0, rough=None, props=(), **hkw):
         """rough: None = flat floor; else (seed, global env id) of the Philox terrain of
-        CreateRoughFloor (Environment.cs:230-261)"""
+        CreateRoughFloor (Environment.cs:230-261).  props: Prop structures appended to the
+        body list after the floor (scene extension)"""
         self.h = hyper(**hkw)
         if rough is None:
             self.p = lib().orc_env_create(C.byref(self.h), float(dx), int(material))
@@ -121,6 +150,9 @@ class Env:
             self._draws = np.array(terrain_draws(*rough), np.int32)
             self.p = lib().orc_env_create_floor(C.byref(self.h), float(dx), int(material),
                                                 _p(self._draws))
+        for pr in props:
+            if lib().orc_env_add_prop(self.p, C.byref(pr)) < 0:
+                raise ValueError("bad prop")
 
     def __del__(self):
         if getattr(self, "p", None):
@@ -161,6 +193,15 @@ class Env:
                 break
             out.append(buf[:2 * nv].reshape(nv, 2).copy())
         return out
+
+    def prop(self, k):
+        """(vertices (n, 2), [cx, cy, vx, vy, w, angle]) of scene prop k"""
+        xy = np.empty(2 * PROP_MAXV, np.float32)
+        st = np.empty(6, np.float32)
+        n = lib().orc_env_prop(self.p, int(k), _p(xy), _p(st))
+        if n == 0:
+            raise IndexError(k)
+        return xy[:2 * n].reshape(n, 2).copy(), st
 
     def joint_step(self, j):
         lib().orc_env_joint_step(self.p, int(j))

@@ -72,7 +72,7 @@ static const material MATS[ORC_NMAT] = {
 /* ---------------- rigid bodies ---------------- */
 typedef struct {
   int nv;
-  v2 v[6];
+  v2 v[ORC_PROP_MAXV];
   v2 centroid;
   int is_static, is_floor, collided;
   float inv_mass, inv_inertia, restitution, friction;
@@ -83,12 +83,13 @@ typedef struct {
 
 typedef struct { int a, b, ia, ib; float torque; } joint;
 
-enum { MAXB = 5 + ORC_ROUGH_SEGMENTS };
+enum { MAXB = 5 + ORC_ROUGH_SEGMENTS + ORC_MAX_PROPS };
 struct orc_env {
   orc_hyper h;
-  body bodies[MAXB];   /* ORC_LLL..ORC_RLU, then the floor body / rough-floor segments */
+  body bodies[MAXB];   /* ORC_LLL..ORC_RLU, the floor body / rough-floor segments, props */
   int order[MAXB];     /* List<RigidBody> order */
-  int nbodies;         /* 6, or 15 with the rough floor */
+  int nbodies;         /* 6, or 15 with the rough floor, + props */
+  int nprops;
   int rough;
   joint joints[4];
   v2 position, prev_position;
@@ -398,7 +399,8 @@ static void resolve_collisions(orc_env* e, int self, orc_pair_trace* tr) {
     if (is_assoc(A, o)) continue;
     body* B = &e->bodies[o];
     if (!aabb_overlap(A, B)) continue;
-    int pi = e->rough ? (o < ORC_FLOOR ? PAIR_IDX[self][o] : -1) : PAIR_IDX[self][o];
+    /* traced pairs: the walker's own 9 candidates (the flat floor's, not a segment's or a prop's) */
+    int pi = (self < ORC_FLOOR && o < ORC_FLOOR + (e->rough ? 0 : 1)) ? PAIR_IDX[self][o] : -1;
     if (tr && pi >= 0) tr->aabb_hit[pi] = 1;
     if (B->is_floor) A->collided = 1;
     if (A->is_floor) B->collided = 1;
@@ -528,6 +530,18 @@ void orc_env_get_obs(const orc_env* e, float s[12]) {
 
 static void initial_state(orc_env* e) { walker_update(e); }
 
+/* List<RigidBody> order.  Episode 0: the walker (CreateCreature), then the floor body /
+ * segments (CreateFloor), then the scene props in the order they were added.  After a
+ * reset the walker's five bodies are removed and re-appended (Walker.Reset / RemoveRigidObjects,
+ * Walker.cs:212-234): the floor bodies and props keep their relative order in front. */
+static void build_order(orc_env* e) {
+  const int nf = e->nbodies - 5;
+  const int w0 = e->post_reset ? nf : 0, f0 = e->post_reset ? 0 : 5;
+  e->order[w0 + 0] = ORC_LLL; e->order[w0 + 1] = ORC_LLU; e->order[w0 + 2] = ORC_BODY;
+  e->order[w0 + 3] = ORC_RLL; e->order[w0 + 4] = ORC_RLU;
+  for (int k = 0; k < nf; k++) e->order[f0 + k] = ORC_FLOOR + k;
+}
+
 void orc_env_reset(orc_env* e) {
   /* Environment.Reset (:167-173) -> Walker.Reset (Walker.cs:212-223): the walker's
    * bodies are removed and re-appended AFTER the floor. */
@@ -536,11 +550,8 @@ void orc_env_reset(orc_env* e) {
   e->position = V(125.0f + e->dx, 800.0f);
   e->prev_position = e->position;
   create_creature(e);
-  const int nf = e->nbodies - 5;  /* the floor body / segments keep their list positions */
-  for (int k = 0; k < nf; k++) e->order[k] = ORC_FLOOR + k;
-  e->order[nf + 0] = ORC_LLL; e->order[nf + 1] = ORC_LLU; e->order[nf + 2] = ORC_BODY;
-  e->order[nf + 3] = ORC_RLL; e->order[nf + 4] = ORC_RLU;
   e->post_reset = 1;
+  build_order(e);
   initial_state(e);
 }
 
@@ -593,12 +604,93 @@ orc_env* orc_env_create_floor(const orc_hyper* h, float dx, int material, const 
     v2 fl[4] = {V(-50, 1050), V(-50, 900), V(1050, 900), V(1050, 1050)};
     body_init(&e->bodies[ORC_FLOOR], ORC_MAT_METAL, fl, 4, 1, 1);
   }
-  e->order[0] = ORC_LLL; e->order[1] = ORC_LLU; e->order[2] = ORC_BODY;
-  e->order[3] = ORC_RLL; e->order[4] = ORC_RLU;
-  for (int k = 5; k < e->nbodies; k++) e->order[k] = k;
   e->post_reset = 0;
+  build_order(e);
   initial_state(e);
   return e;
+}
+
+/* ---------------- scene props (Objects/RigidBodies/{Square,Triangle,Hexagon}.cs) ----------------
+ * FromSize(material, centroid, size, isStatic): adjustment = (float)0.5 * size, vertices in
+ * the listed order; RigidBody ctor (RigidBody.cs:36-50); then, as a caller would,
+ * SmoothCorners(count) (Skeleton.cs:33-53: the vertex list is replaced, the centroid is NOT
+ * recomputed), SetLinearVelocity / SetAngularVelocity / AddAcceleration (:143-183). */
+int orc_prop_vertices(const orc_prop* p, float* xy) {
+  const v2 c = V(p->cx, p->cy);
+  const float adj = (float)0.5 * p->size;
+  v2 vs[ORC_PROP_MAXV];
+  int n;
+  if (p->shape == ORC_SHAPE_SQUARE) {        /* Square.cs:18-31 */
+    vs[0] = V(c.x + adj, c.y + adj); vs[1] = V(c.x - adj, c.y + adj);
+    vs[2] = V(c.x - adj, c.y - adj); vs[3] = V(c.x + adj, c.y - adj);
+    n = 4;
+  } else if (p->shape == ORC_SHAPE_TRIANGLE) {  /* Triangle.cs:18-30 */
+    vs[0] = V(c.x, c.y + adj); vs[1] = V(c.x - adj, c.y - adj); vs[2] = V(c.x + adj, c.y - adj);
+    n = 3;
+  } else if (p->shape == ORC_SHAPE_HEXAGON) {   /* Hexagon.cs:18-33 */
+    vs[0] = V(c.x + (adj * 0.5f), c.y + adj); vs[1] = V(c.x - (adj * 0.5f), c.y + adj);
+    vs[2] = V(c.x - adj, c.y);                 vs[3] = V(c.x - (adj * 0.5f), c.y - adj);
+    vs[4] = V(c.x + (adj * 0.5f), c.y - adj); vs[5] = V(c.x + adj, c.y);
+    n = 6;
+  } else {
+    return -1;
+  }
+  if (p->smooth < 0) return -1;
+  for (int it = 0; it < p->smooth; it++) {   /* SmoothCorners(count) */
+    if (2 * n > ORC_PROP_MAXV) return -1;
+    v2 nv[ORC_PROP_MAXV];
+    for (int j = 0; j < n; j++) {
+      v2 faceAB = vsub(vs[(j + 1) % n], vs[j]);
+      faceAB = vmul(faceAB, 0.2f);
+      v2 faceAC = vsub(vs[mod_ref((float)(j - 1), (float)n)], vs[j]);
+      faceAC = vmul(faceAC, 0.2f);
+      nv[2 * j] = vadd(vs[j], faceAC);
+      nv[2 * j + 1] = vadd(vs[j], faceAB);
+    }
+    n *= 2;
+    memcpy(vs, nv, sizeof(v2) * (size_t)n);
+  }
+  if (xy)
+    for (int i = 0; i < n; i++) { xy[2 * i] = vs[i].x; xy[2 * i + 1] = vs[i].y; }
+  return n;
+}
+
+int orc_env_add_prop(orc_env* e, const orc_prop* p) {
+  if (e->nprops >= ORC_MAX_PROPS || p->material < 0 || p->material >= ORC_NMAT) return -1;
+  float xy[2 * ORC_PROP_MAXV];
+  const int n = orc_prop_vertices(p, xy);
+  if (n < 3) return -1;
+  /* the centroid of FromSize's vertices (AddVectors), before SmoothCorners */
+  orc_prop base = *p;
+  base.smooth = 0;
+  float bxy[2 * ORC_PROP_MAXV];
+  const int nb = orc_prop_vertices(&base, bxy);
+  v2 bv[ORC_PROP_MAXV];
+  for (int i = 0; i < nb; i++) bv[i] = V(bxy[2 * i], bxy[2 * i + 1]);
+  body* b = &e->bodies[e->nbodies];
+  body_init(b, p->material, bv, nb, p->is_static != 0, 0);
+  b->nv = n;
+  for (int i = 0; i < n; i++) b->v[i] = V(xy[2 * i], xy[2 * i + 1]);
+  b->lin_vel = V(p->vx, p->vy);
+  b->ang_vel = p->w;
+  b->accel = vadd(b->accel, V(p->ax, p->ay));
+  e->nbodies++;
+  e->nprops++;
+  build_order(e);
+  return e->nprops - 1;
+}
+
+/* prop k: vertices (x0, y0, ...) and {cx, cy, vx, vy, w, angle}; returns the vertex count */
+int orc_env_prop(const orc_env* e, int k, float* xy, float st[6]) {
+  if (k < 0 || k >= e->nprops) return 0;
+  const body* b = &e->bodies[e->nbodies - e->nprops + k];
+  if (xy)
+    for (int i = 0; i < b->nv; i++) { xy[2 * i] = b->v[i].x; xy[2 * i + 1] = b->v[i].y; }
+  if (st) {
+    st[0] = b->centroid.x; st[1] = b->centroid.y; st[2] = b->lin_vel.x; st[3] = b->lin_vel.y;
+    st[4] = b->ang_vel; st[5] = b->angle;
+  }
+  return b->nv;
 }
 
 orc_env* orc_env_create(const orc_hyper* h, float dx, int material) {
@@ -607,7 +699,7 @@ orc_env* orc_env_create(const orc_hyper* h, float dx, int material) {
 
 /* floor body k's vertices (x0, y0, x1, y1, ...); returns the vertex count */
 int orc_env_floor_body(const orc_env* e, int k, float* xy) {
-  if (k < 0 || k >= e->nbodies - 5) return 0;
+  if (k < 0 || k >= e->nbodies - 5 - e->nprops) return 0;
   const body* b = &e->bodies[ORC_FLOOR + k];
   for (int i = 0; i < b->nv; i++) { xy[2 * i] = b->v[i].x; xy[2 * i + 1] = b->v[i].y; }
   return b->nv;

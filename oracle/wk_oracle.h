@@ -38,7 +38,9 @@ enum {
   ORC_ST_TERMINAL = 110,  /* Walker.Terminal */
   ORC_ST_EPISODES = 111,  /* completed episodes */
   ORC_STATE_FLOATS = 112,
-  ORC_ROUGH_SEGMENTS = 10  /* CreateRoughFloor(segments = 10) */
+  ORC_ROUGH_SEGMENTS = 10, /* CreateRoughFloor(segments = 10) */
+  ORC_MAX_PROPS = 4,       /* scene props (extension: Square / Triangle / Hexagon bodies) */
+  ORC_PROP_MAXV = 24       /* vertices of one prop after SmoothCorners */
 };
 
 /* candidate pair checks per substep, canonical index (this, other):
@@ -90,6 +92,16 @@ orc_env* orc_env_create_floor(const orc_hyper* h, float dx, int material, const 
 int orc_env_floor_body(const orc_env* e, int k, float* xy);
 int orc_terrain_draw(uint64_t seed, int env, int i);
 void orc_env_destroy(orc_env* e);
+/* scene props: Square / Triangle / Hexagon.FromSize (+ SmoothCorners, velocities,
+ * acceleration) appended to the body list after the floor; same layout as wk_prop */
+enum { ORC_SHAPE_SQUARE = 0, ORC_SHAPE_TRIANGLE = 1, ORC_SHAPE_HEXAGON = 2 };
+typedef struct {
+  int32_t shape, smooth, material, is_static;
+  float cx, cy, size, vx, vy, w, ax, ay;
+} orc_prop;
+int orc_prop_vertices(const orc_prop* p, float* xy);
+int orc_env_add_prop(orc_env* e, const orc_prop* p);
+int orc_env_prop(const orc_env* e, int k, float* xy, float st[6]);
 /* one Environment.Update with a given (unclipped) action; clip as Environment.cs:78.
  * obs: 12 floats after the step (after auto-reset if done). trace: per-substep pair
  * trace array of h->Iterations entries (may be NULL). */

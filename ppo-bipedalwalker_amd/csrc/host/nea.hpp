@@ -70,6 +70,46 @@ NEA_MATERIAL(SuperRubber, WK_MAT_SUPERRUBBER, 11.0f, 1.0f, 1.0f)
 #undef NEA_MATERIAL
 }  // namespace Materials
 
+namespace Objects {
+namespace RigidBodies {
+// Square / Triangle / Hexagon (Objects/RigidBodies/<Shape>.cs): FromSize builds the
+// description of one scene prop; the RigidBody setters the reference offers before the body
+// joins the list (RigidBody.cs:143-189) fill in the rest.  Environment::AddRigidBodies
+// hands them to every walker (wk_set_scene).
+class Prop {
+ public:
+  Prop& SmoothCorners(int count = 1) { p_.smooth += count; return *this; }
+  Prop& SetLinearVelocity(float x, float y) { p_.vx = x; p_.vy = y; return *this; }
+  Prop& SetAngularVelocity(float w) { p_.w = w; return *this; }
+  Prop& AddAcceleration(float x, float y) { p_.ax = p_.ax + x; p_.ay = p_.ay + y; return *this; }
+  const wk_prop& Desc() const { return p_; }
+
+ protected:
+  Prop(int shape, const Materials::IMaterial& m, float cx, float cy, float size, bool isStatic) {
+    p_.shape = shape; p_.smooth = 0; p_.material = m.Id(); p_.is_static = isStatic ? 1 : 0;
+    p_.cx = cx; p_.cy = cy; p_.size = size;
+    p_.vx = p_.vy = p_.w = p_.ax = p_.ay = 0.0f;
+  }
+  wk_prop p_{};
+};
+#define NEA_SHAPE(Name, id)                                                                   \
+  struct Name : Prop {                                                                        \
+    static Name FromSize(const Materials::IMaterial& m, float cx, float cy, float size,       \
+                         bool isStatic = false) {                                             \
+      return Name(m, cx, cy, size, isStatic);                                                 \
+    }                                                                                         \
+                                                                                              \
+   private:                                                                                   \
+    Name(const Materials::IMaterial& m, float cx, float cy, float size, bool st)              \
+        : Prop(id, m, cx, cy, size, st) {}                                                    \
+  };
+NEA_SHAPE(Square, WK_SHAPE_SQUARE)
+NEA_SHAPE(Triangle, WK_SHAPE_TRIANGLE)
+NEA_SHAPE(Hexagon, WK_SHAPE_HEXAGON)
+#undef NEA_SHAPE
+}  // namespace RigidBodies
+}  // namespace Objects
+
 namespace Walker {
 namespace PPO {
 // Hyperparameters (Hyperparameters.cs:80-121): static-like defaults as a value type
@@ -205,6 +245,12 @@ class Environment {
   void StepObjects(const std::vector<float>& actions) {
     pending_ = actions;
     Update(1.0f);
+  }
+  // _rigidBodies.Add(...) after CreateFloor() (Environment.cs:39-51) for every walker
+  void AddRigidBodies(const std::vector<Objects::RigidBodies::Prop>& props) {
+    std::vector<wk_prop> d;
+    for (const auto& p : props) d.push_back(p.Desc());
+    if (wk_set_scene(ctx_, d.data(), (int)d.size()) != WK_OK) LogError(wk_last_error(ctx_));
   }
   // InitialState (:176-180)
   void InitialState() {

@@ -72,6 +72,10 @@ struct wk_ctx {
   float* partial = nullptr; size_t partial_floats = 0;
   void* scratch = nullptr; size_t scratch_bytes = 0;
   void* scratch2 = nullptr; size_t scratch2_bytes = 0;
+  // scene props (wk_set_scene): descriptions, kernel constants, [n][pstride] state
+  std::vector<wk_prop> scene_desc;
+  wk::SceneDev scene{};
+  float* props = nullptr;
   // comm
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
@@ -355,7 +359,7 @@ int wk_destroy(wk_ctx* c) {
   void* bufs[] = {c->st, c->dxoff, c->mat, c->rng_t, c->W, c->Wz, c->m, c->v, c->grad, c->ts, c->ta,
                   c->tlp, c->tr, c->tv, c->tret, c->tadv, c->td, c->partial, c->scratch, c->scratch2,
                   c->ep_acc, c->ep_len, c->ep_scratch, c->ep_rowcnt, c->ep_count, c->ep_log,
-                  c->loss_log};
+                  c->loss_log, c->props};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -400,6 +404,15 @@ int wk_set_offsets(wk_ctx* c, const float* dx) {
   return WK_OK;
 }
 
+// the env-step kernel of the context's mapping; with scene props the one-lane scene kernel
+static hipError_t launch_physics(wk_ctx* c, int mode, wk::StepArgs& A) {
+  if (c->scene.n_props > 0) {
+    A.props = c->props;
+    return wk::launch_env_scene(mode, c->P, A, c->scene, c->stream);
+  }
+  return wk::launch_env_step(mode, c->P, A, c->stream);
+}
+
 static int step_impl(wk_ctx* c, const float* d_actions, int k, float* d_obs, float* d_rew,
                      uint8_t* d_done, uint32_t* d_fault, int mode, void* trace) {
   wk::StepArgs A{};
@@ -411,7 +424,7 @@ static int step_impl(wk_ctx* c, const float* d_actions, int k, float* d_obs, flo
   A.trace = (wk::PairTraceDev*)trace;
   A.k_steps = k;
   ProfScope ps(c, PK_PHYS, (int64_t)k * c->n);
-  HIPCHK(c, wk::launch_env_step(mode, c->P, A, c->stream));
+  HIPCHK(c, launch_physics(c, mode, A));
   return WK_OK;
 }
 
@@ -534,6 +547,141 @@ int wk_get_body_view(wk_ctx* c, int env, int body, wk_body_view* o) {
   return WK_OK;
 }
 
+// ---------------- scene props (wk_scene.inc) ----------------
+// <Shape>.FromSize (Square.cs:18-31, Triangle.cs:18-30, Hexagon.cs:18-33) then
+// Skeleton.SmoothCorners (Skeleton.cs:33-53) in host fp32 (built with -ffp-contract=off,
+// the same IEEE ops as the oracle); returns the vertex count or -1
+static int prop_vertices(const wk_prop& p, int smooth, float* xs, float* ys) {
+  const float cx = p.cx, cy = p.cy, adj = (float)0.5 * p.size;
+  int n;
+  if (p.shape == WK_SHAPE_SQUARE) {
+    const float vx[4] = {cx + adj, cx - adj, cx - adj, cx + adj};
+    const float vy[4] = {cy + adj, cy + adj, cy - adj, cy - adj};
+    n = 4;
+    for (int i = 0; i < n; i++) { xs[i] = vx[i]; ys[i] = vy[i]; }
+  } else if (p.shape == WK_SHAPE_TRIANGLE) {
+    const float vx[3] = {cx, cx - adj, cx + adj};
+    const float vy[3] = {cy + adj, cy - adj, cy - adj};
+    n = 3;
+    for (int i = 0; i < n; i++) { xs[i] = vx[i]; ys[i] = vy[i]; }
+  } else if (p.shape == WK_SHAPE_HEXAGON) {
+    const float h = adj * 0.5f;
+    const float vx[6] = {cx + h, cx - h, cx - adj, cx - h, cx + h, cx + adj};
+    const float vy[6] = {cy + adj, cy + adj, cy, cy - adj, cy - adj, cy};
+    n = 6;
+    for (int i = 0; i < n; i++) { xs[i] = vx[i]; ys[i] = vy[i]; }
+  } else {
+    return -1;
+  }
+  for (int it = 0; it < smooth; it++) {
+    if (2 * n > WK_PROP_MAXV) return -1;
+    float nx[WK_PROP_MAXV], ny[WK_PROP_MAXV];
+    for (int j = 0; j < n; j++) {
+      const int a = (j + 1) % n, b = (j + n - 1) % n;  // ContactPoints.Mod(j - 1, n)
+      const float abx = (xs[a] - xs[j]) * 0.2f, aby = (ys[a] - ys[j]) * 0.2f;
+      const float acx = (xs[b] - xs[j]) * 0.2f, acy = (ys[b] - ys[j]) * 0.2f;
+      nx[2 * j] = xs[j] + acx; ny[2 * j] = ys[j] + acy;
+      nx[2 * j + 1] = xs[j] + abx; ny[2 * j + 1] = ys[j] + aby;
+    }
+    n *= 2;
+    for (int i = 0; i < n; i++) { xs[i] = nx[i]; ys[i] = ny[i]; }
+  }
+  return n;
+}
+
+static const float kMatProps[8][3] = {  // Materials/*.cs: inverse mass, restitution, friction
+    {5.0f, 0.3f, 0.8f}, {11.0f, 0.3f, 0.0f}, {11.0f, 0.7f, 0.5f}, {15.0f, 0.3f, 1.0f},
+    {20.0f, 0.3f, 0.01f}, {1.0f, 0.3f, 0.1f}, {0.01f, 0.1f, 0.2f}, {11.0f, 1.0f, 1.0f}};
+
+int wk_set_scene(wk_ctx* c, const wk_prop* props, int n_props) {
+  if (!c || n_props < 0 || (n_props > 0 && !props)) return WK_ERR_ARG;
+  if (n_props > WK_MAX_PROPS) { SETERR(c, "at most %d scene props", (int)WK_MAX_PROPS); return WK_ERR_ARG; }
+  if (n_props > 0 && c->P.rough) { SETERR(c, "scene props run with the flat floor (RoughFloor = 0)"); return WK_ERR_CONFIG; }
+  if (n_props > 0 && c->cfg.LanesPerWalker > 1) {
+    SETERR(c, "scene props run on the one-lane mapping (LanesPerWalker 0 or 1)");
+    return WK_ERR_CONFIG;
+  }
+  wk::SceneDev S{};
+  std::vector<float> rec;
+  for (int k = 0; k < n_props; k++) {
+    const wk_prop& p = props[k];
+    const float fin[8] = {p.cx, p.cy, p.size, p.vx, p.vy, p.w, p.ax, p.ay};
+    for (float f : fin)
+      if (!std::isfinite(f)) { SETERR(c, "prop %d: non-finite parameter", k); return WK_ERR_ARG; }
+    if (p.material < 0 || p.material > 7 || p.smooth < 0 || !(p.size > 0.0f)) {
+      SETERR(c, "prop %d: invalid material, smooth count or size", k);
+      return WK_ERR_ARG;
+    }
+    float xs[WK_PROP_MAXV], ys[WK_PROP_MAXV], bx[WK_PROP_MAXV], by[WK_PROP_MAXV];
+    const int nv = prop_vertices(p, p.smooth, xs, ys);
+    if (nv < 0) { SETERR(c, "prop %d: unknown shape or more than %d vertices", k, (int)WK_PROP_MAXV); return WK_ERR_ARG; }
+    if ((int)rec.size() + 2 * nv + 6 > wk::SCENE_FIELDS) {
+      SETERR(c, "scene props exceed %d vertices in total", (int)WK_SCENE_MAX_VERTS);
+      return WK_ERR_ARG;
+    }
+    int total = nv;
+    for (int j = 0; j < k; j++) total += S.nv[j];
+    if (total > WK_SCENE_MAX_VERTS) { SETERR(c, "scene props exceed %d vertices in total", (int)WK_SCENE_MAX_VERTS); return WK_ERR_ARG; }
+    // Skeleton.AddVectors -> FindCentroid of the FromSize vertices (before SmoothCorners)
+    const int nb = prop_vertices(p, 0, bx, by);
+    float sx = 0.0f, sy = 0.0f;
+    for (int i = 0; i < nb; i++) { sx = sx + bx[i]; sy = sy + by[i]; }
+    const float inv = 1.0f / (float)nb;
+    S.nv[k] = nv;
+    S.off[k] = (int)rec.size();
+    S.stat[k] = p.is_static ? 1 : 0;
+    // RigidBody ctor (RigidBody.cs:36-50)
+    S.im[k] = p.is_static ? 0.0f : kMatProps[p.material][0];
+    S.ii[k] = p.is_static ? 0.0f : 0.001f * kMatProps[p.material][0];
+    S.e[k] = kMatProps[p.material][1];
+    S.mu[k] = kMatProps[p.material][2];
+    S.adx[k] = p.ax * c->P.dt_sub;  // _acceleration * deltaTime (StepLinearVelocity)
+    S.ady[k] = p.ay * c->P.dt_sub;
+    for (int i = 0; i < nv; i++) rec.push_back(xs[i]);
+    for (int i = 0; i < nv; i++) rec.push_back(ys[i]);
+    const float tail[6] = {sx * inv, sy * inv, p.vx, p.vy, p.w, 0.0f};
+    for (float f : tail) rec.push_back(f);
+  }
+  S.n_props = n_props;
+  S.pstride = (int)rec.size();
+  float* dev = nullptr;
+  if (n_props > 0) {
+    std::vector<float> all((size_t)c->n * rec.size());
+    for (int e = 0; e < c->n; e++) memcpy(all.data() + (size_t)e * rec.size(), rec.data(), sizeof(float) * rec.size());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMalloc(&dev, sizeof(float) * all.size()));
+    if (hipMemcpy(dev, all.data(), sizeof(float) * all.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(dev);
+      SETERR(c, "scene upload failed");
+      return WK_ERR_HIP;
+    }
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->props) (void)hipFree(c->props);
+  c->props = dev;
+  c->scene = S;
+  c->scene_desc.assign(props, props + n_props);
+  return WK_OK;
+}
+
+int wk_get_prop_view(wk_ctx* c, int env, int k, wk_prop_view* o) {
+  if (!c || !o || env < 0 || env >= c->n || k < 0 || k >= c->scene.n_props) return WK_ERR_ARG;
+  memset(o, 0, sizeof(*o));
+  const int nv = c->scene.nv[k];
+  std::vector<float> f(2 * nv + 6);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(f.data(), c->props + (size_t)env * c->scene.pstride + c->scene.off[k],
+                      sizeof(float) * f.size(), hipMemcpyDeviceToHost));
+  o->n_vertices = nv;
+  for (int i = 0; i < nv; i++) { o->vertices[i][0] = f[i]; o->vertices[i][1] = f[nv + i]; }
+  o->centroid[0] = f[2 * nv]; o->centroid[1] = f[2 * nv + 1];
+  o->linear_velocity[0] = f[2 * nv + 2]; o->linear_velocity[1] = f[2 * nv + 3];
+  o->angular_velocity = f[2 * nv + 4];
+  o->angle = f[2 * nv + 5];
+  o->is_static = c->scene.stat[k];
+  return WK_OK;
+}
+
 int wk_get_weights(wk_ctx* c, float* p) {
   if (!c || !p) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -629,7 +777,7 @@ int wk_rollout(wk_ctx* c, int horizon) {
   A.traj_v = c->tv; A.t0 = 0; A.k_steps = horizon;
   {
     ProfScope ps(c, PK_PHYS, (int64_t)horizon * c->n);
-    HIPCHK(c, wk::launch_env_step(3, c->P, A, c->stream));
+    HIPCHK(c, launch_physics(c, 3, A));
   }
   c->T_valid = horizon;
   if (c->collect) {
@@ -1040,7 +1188,7 @@ struct CkptHeader {
   uint32_t rollout_steps;
 };
 static_assert(sizeof(CkptHeader) == 48, "checkpoint header");
-const uint32_t kCkptVersion = 2;
+const uint32_t kCkptVersion = 3;  // 3: + scene section (int32 n_props, wk_prop[n_props], [n][pstride])
 size_t ckpt_bytes(size_t n) {
   return sizeof(CkptHeader) + sizeof(float) * (3 * wk::NPARAM + n * wk::NSTATE + 2 * n) +
          sizeof(int32_t) * n + sizeof(double) * n + sizeof(int32_t) * n;
@@ -1109,7 +1257,9 @@ int wk_checkpoint_save(wk_ctx* c, const char* path) {
   CkptHeader h{kCkptMagic, kCkptVersion, (uint32_t)n, (uint32_t)wk::NSTATE, (uint32_t)wk::NPARAM,
                (uint32_t)c->adam_t, c->seed, c->cfg.EnvOffset, c->cfg.Iterations,
                c->cfg.MaxTimesteps, c->rollout_steps};
-  std::vector<char> buf(ckpt_bytes(n));
+  const int np = c->scene.n_props;
+  const size_t scene_bytes = sizeof(int32_t) + sizeof(wk_prop) * np + sizeof(float) * n * c->scene.pstride;
+  std::vector<char> buf(ckpt_bytes(n) + scene_bytes);
   char* q = buf.data();
   memcpy(q, &h, sizeof h); q += sizeof h;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1121,7 +1271,13 @@ int wk_checkpoint_save(wk_ctx* c, const char* path) {
   HIPCHK(c, hipMemcpy(q, c->dxoff, sizeof(float) * n, hipMemcpyDeviceToHost)); q += sizeof(float) * n;
   HIPCHK(c, hipMemcpy(q, c->mat, sizeof(int32_t) * n, hipMemcpyDeviceToHost)); q += sizeof(int32_t) * n;
   HIPCHK(c, hipMemcpy(q, c->ep_acc, sizeof(double) * n, hipMemcpyDeviceToHost)); q += sizeof(double) * n;
-  HIPCHK(c, hipMemcpy(q, c->ep_len, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(q, c->ep_len, sizeof(int32_t) * n, hipMemcpyDeviceToHost)); q += sizeof(int32_t) * n;
+  const int32_t np32 = np;
+  memcpy(q, &np32, sizeof np32); q += sizeof np32;
+  if (np > 0) {
+    memcpy(q, c->scene_desc.data(), sizeof(wk_prop) * np); q += sizeof(wk_prop) * np;
+    HIPCHK(c, hipMemcpy(q, c->props, sizeof(float) * n * c->scene.pstride, hipMemcpyDeviceToHost));
+  }
   if (!write_file(path, buf.data(), buf.size())) { SETERR(c, "cannot write checkpoint '%s'", path); return WK_ERR_ARG; }
   return WK_OK;
 }
@@ -1134,7 +1290,24 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
   CkptHeader h;
   if (data.size() < sizeof h) { SETERR(c, "checkpoint '%s' truncated", path); return WK_ERR_ARG; }
   memcpy(&h, data.data(), sizeof h);
-  const size_t need = ckpt_bytes(n);
+  size_t need = ckpt_bytes(n) + sizeof(int32_t);
+  int32_t np = 0;
+  std::vector<wk_prop> desc;
+  if (data.size() >= need) {
+    memcpy(&np, data.data() + need - sizeof(int32_t), sizeof np);
+    if (np > 0 && np <= WK_MAX_PROPS && data.size() >= need + sizeof(wk_prop) * np) {
+      desc.resize(np);
+      memcpy(desc.data(), data.data() + need, sizeof(wk_prop) * np);
+      need += sizeof(wk_prop) * np;
+      size_t pstride = 0;
+      for (const wk_prop& p : desc) {
+        float xs[WK_PROP_MAXV], ys[WK_PROP_MAXV];
+        const int nv = p.smooth >= 0 ? prop_vertices(p, p.smooth, xs, ys) : -1;
+        pstride += nv > 0 ? (size_t)(2 * nv + 6) : (size_t)1 << 40;  // a bad record fails the size check
+      }
+      need += sizeof(float) * n * pstride;
+    }
+  }
   if (h.magic != kCkptMagic || h.version != kCkptVersion) { SETERR(c, "'%s' is not a wk checkpoint", path); return WK_ERR_ARG; }
   if (h.n_env != n || h.nstate != (uint32_t)wk::NSTATE || h.nparam != (uint32_t)wk::NPARAM || data.size() != need) {
     SETERR(c, "checkpoint '%s' is for %u walkers (context has %zu)", path, h.n_env, n);
@@ -1155,7 +1328,13 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
   HIPCHK(c, hipMemcpy(c->dxoff, q, sizeof(float) * n, hipMemcpyHostToDevice)); q += sizeof(float) * n;
   HIPCHK(c, hipMemcpy(c->mat, q, sizeof(int32_t) * n, hipMemcpyHostToDevice)); q += sizeof(int32_t) * n;
   HIPCHK(c, hipMemcpy(c->ep_acc, q, sizeof(double) * n, hipMemcpyHostToDevice)); q += sizeof(double) * n;
-  HIPCHK(c, hipMemcpy(c->ep_len, q, sizeof(int32_t) * n, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->ep_len, q, sizeof(int32_t) * n, hipMemcpyHostToDevice)); q += sizeof(int32_t) * n;
+  // the scene: rebuilt from its descriptions, then every walker's saved prop state
+  if (int r = wk_set_scene(c, desc.data(), (int)desc.size()); r != WK_OK) return r;
+  if (np > 0) {
+    q += sizeof(int32_t) + sizeof(wk_prop) * np;
+    HIPCHK(c, hipMemcpy(c->props, q, sizeof(float) * n * c->scene.pstride, hipMemcpyHostToDevice));
+  }
   c->adam_t = (int)h.adam_t;
   c->rollout_steps = h.rollout_steps;
   c->T_valid = 0;

@@ -41,6 +41,21 @@ struct StepArgs {
   int t0;
   PairTraceDev* trace;       // [n][iterations] (TRACE)
   int k_steps;
+  float* props;              // scene props [n][SceneDev::pstride] (k_env_scene) or null
+};
+
+// scene props (wk_scene.inc): Square / Triangle / Hexagon bodies after the floor, the same
+// shapes for every walker; per walker and prop k the state x[nv], y[nv], cx, cy, vx, vy, w,
+// angle starts at float off[k] of the walker's prop record
+enum : int {
+  SCENE_MAX_PROPS = 4, SCENE_PROP_MAXV = 24, SCENE_MAX_VERTS = 32,
+  SCENE_FIELDS = 2 * SCENE_MAX_VERTS + 6 * SCENE_MAX_PROPS
+};
+struct SceneDev {
+  int n_props, pstride;
+  int nv[SCENE_MAX_PROPS], off[SCENE_MAX_PROPS], stat[SCENE_MAX_PROPS];
+  float im[SCENE_MAX_PROPS], ii[SCENE_MAX_PROPS], e[SCENE_MAX_PROPS], mu[SCENE_MAX_PROPS];
+  float adx[SCENE_MAX_PROPS], ady[SCENE_MAX_PROPS];  // acceleration * deltaTime
 };
 
 struct GradArgs {
@@ -73,6 +88,8 @@ struct AdamArgs {
 enum : int { SLAB = NPARAM + 4 };  // gradient + critic diag, actor diag, skipped, pad
 
 hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s);
+hipError_t launch_env_scene(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
+                            hipStream_t s);
 hipError_t launch_env_init(const EnvParams& P, float* st, const float* dx, const uint8_t* mask,
                            int post, hipStream_t s);
 hipError_t launch_get_obs(const EnvParams& P, const float* st, float* obs, hipStream_t s);

@@ -1178,6 +1178,10 @@ __global__ void k_returns(int n, int T, int use_gae, float gamma, float lambda,
 
 }  // namespace wk
 
+namespace wk {
+#include "wk_scene.inc"
+}  // namespace wk
+
 // host-side launch shims (C++ linkage, used by wk_api.cpp)
 namespace wk {
 template <int L, bool ROUGH>
@@ -1203,6 +1207,17 @@ static void launch_side(int mode, const EnvParams& P, const StepArgs& A, hipStre
     case 2: hipLaunchKernelGGL((k_env_side<true, false, false>), grd, blk, 0, s, P, A); break;
     default: hipLaunchKernelGGL((k_env_side<true, true, false>), grd, blk, 0, s, P, A); break;
   }
+}
+hipError_t launch_env_scene(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
+                            hipStream_t s) {
+  dim3 blk(64), grd((unsigned)((P.n_env + 63) / 64));
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((k_env_scene<false, false, false>), grd, blk, 0, s, P, A, S); break;
+    case 1: hipLaunchKernelGGL((k_env_scene<false, false, true>), grd, blk, 0, s, P, A, S); break;
+    case 2: hipLaunchKernelGGL((k_env_scene<true, false, false>), grd, blk, 0, s, P, A, S); break;
+    default: hipLaunchKernelGGL((k_env_scene<true, true, false>), grd, blk, 0, s, P, A, S); break;
+  }
+  return hipGetLastError();
 }
 hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
   if (P.lanes == 2) launch_side(mode, P, A, s);

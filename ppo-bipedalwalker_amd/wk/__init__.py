@@ -27,7 +27,7 @@ EXPORTS = [
     "wk_config_defaults", "wk_version", "wk_create", "wk_destroy", "wk_last_error", "wk_sync",
     "wk_num_envs", "wk_reset", "wk_set_materials", "wk_set_offsets", "wk_step",
     "wk_step_device", "wk_step_traced", "wk_get_obs", "wk_get_state", "wk_set_state",
-    "wk_get_body_view", "wk_get_weights", "wk_set_weights", "wk_get_adam", "wk_set_adam",
+    "wk_get_body_view", "wk_set_scene", "wk_get_prop_view", "wk_get_weights", "wk_set_weights", "wk_get_adam", "wk_set_adam",
     "wk_policy_sample", "wk_value", "wk_rollout", "wk_rollout_stats_get", "wk_get_trajectory",
     "wk_set_trajectory", "wk_compute_returns", "wk_ppo_update", "wk_train_batch",
     "wk_minibatch_gradient", "wk_save_weights", "wk_load_weights", "wk_format_weights",
@@ -98,6 +98,33 @@ class BodyView(C.Structure):
                 ("is_static", C.c_int)]
 
 
+SHAPES = {"Square": 0, "Triangle": 1, "Hexagon": 2}
+MAX_PROPS, PROP_MAXV, SCENE_MAX_VERTS = 4, 24, 32
+
+
+class Prop(C.Structure):
+    """wk_prop: <Shape>.FromSize + SmoothCorners + velocities + acceleration (include/wk_api.h)"""
+    _fields_ = [("shape", C.c_int32), ("smooth", C.c_int32), ("material", C.c_int32),
+                ("is_static", C.c_int32), ("cx", C.c_float), ("cy", C.c_float),
+                ("size", C.c_float), ("vx", C.c_float), ("vy", C.c_float), ("w", C.c_float),
+                ("ax", C.c_float), ("ay", C.c_float)]
+
+
+def make_prop(shape="Square", smooth=0, material="Wood", is_static=False, cx=0.0, cy=0.0,
+              size=40.0, vx=0.0, vy=0.0, w=0.0, ax=0.0, ay=0.0):
+    return Prop(SHAPES.get(shape, shape), int(smooth), MATERIALS.get(material, material),
+                int(bool(is_static)), cx, cy, size, vx, vy, w, ax, ay)
+
+
+class PropView(C.Structure):
+    _fields_ = [("n_vertices", C.c_int), ("vertices", (C.c_float * 2) * PROP_MAXV),
+                ("centroid", C.c_float * 2), ("linear_velocity", C.c_float * 2),
+                ("angular_velocity", C.c_float), ("angle", C.c_float), ("is_static", C.c_int)]
+
+    def vertex_array(self):
+        return np.array(self.vertices, np.float32)[:self.n_vertices]
+
+
 class PpoArgs(C.Structure):
     _fields_ = [("epochs", C.c_int), ("minibatch", C.c_int), ("minibatch_global", C.c_int),
                 ("update_index", C.c_uint32)]
@@ -163,6 +190,8 @@ def load_library(path=None):
         "wk_get_state": (I, [P, P]),
         "wk_set_state": (I, [P, P]),
         "wk_get_body_view": (I, [P, I, I, C.POINTER(BodyView)]),
+        "wk_set_scene": (I, [P, P, I]),
+        "wk_get_prop_view": (I, [P, I, I, C.POINTER(PropView)]),
         "wk_get_weights": (I, [P, P]),
         "wk_set_weights": (I, [P, P]),
         "wk_get_adam": (I, [P, P, P, C.POINTER(C.c_int)]),
@@ -402,6 +431,18 @@ class Engine:
         v = BodyView()
         self._chk(self.lib.wk_get_body_view(self.h, int(env), int(body), C.byref(v)),
                   "wk_get_body_view")
+        return v
+
+    def set_scene(self, props):
+        """scene props for every walker (Prop structures / make_prop(...)); [] removes them"""
+        arr = (Prop * max(1, len(props)))(*props)
+        self._chk(self.lib.wk_set_scene(self.h, C.cast(arr, C.c_void_p), len(props)),
+                  "wk_set_scene")
+
+    def prop_view(self, env, k):
+        v = PropView()
+        self._chk(self.lib.wk_get_prop_view(self.h, int(env), int(k), C.byref(v)),
+                  "wk_get_prop_view")
         return v
 
     # -- policy --

@@ -1,7 +1,9 @@
 // Drives the C++ host mirror (csrc/host/nea.hpp) the way the reference's Game1.Update
 // drives Environment.Update, and prints per-step rewards/dones and the final state so
 // tests/test_gpu_parity.py can compare them with the oracle.
-//   test_nea <n_walkers> <steps> <mode: actions|policy> [weights dir: PPOAgent.Save there]
+//   test_nea <n_walkers> <steps> <mode: actions|policy|scene> [weights dir: PPOAgent.Save there]
+// (scene: actions mode with a smoothed Wood box dropped on the walkers and a static
+// Titanium hexagon, added through Environment::AddRigidBodies)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -16,6 +18,13 @@ int main(int argc, char** argv) {
   NEA::Walker::PPO::Hyperparameters h;
   NEA::Materials::Carpet carpet;
   NEA::Environment env(n, h, 20250905, 0, &carpet);
+  if (argc > 3 && strcmp(argv[3], "scene") == 0) {
+    using namespace NEA::Objects::RigidBodies;
+    NEA::Materials::Wood wood;
+    NEA::Materials::Titanium titanium;
+    env.AddRigidBodies({Square::FromSize(wood, 150.0f, 700.0f, 30.0f).SmoothCorners().AddAcceleration(0.0f, 980.0f),
+                        Hexagon::FromSize(titanium, 200.0f, 890.0f, 30.0f, true)});
+  }
   const float dt = h.c.DeltaTime;
   for (int t = 0; t < steps; t++) {
     if (!policy) {

@@ -51,6 +51,32 @@ def test_mirror_matches_oracle(tmp_path, wk, orc):
 
 
 @pytest.mark.gpu
+def test_mirror_scene_matches_oracle(tmp_path, wk, orc):
+    """Square.FromSize(...).SmoothCorners().AddAcceleration(...) and a static Hexagon added
+    through NEA::Environment::AddRigidBodies step like the oracle's props"""
+    exe = build_mirror(tmp_path, wk)
+    n, steps = 4, 60
+    out = subprocess.run([exe, str(n), str(steps), "scene"], capture_output=True, text=True,
+                         check=True, timeout=120).stdout.splitlines()
+    props = [orc.make_prop("Square", 1, "Wood", False, 150, 700, 30, ay=980),
+             orc.make_prop("Hexagon", 0, "Titanium", True, 200, 890, 30)]
+    envs = [orc.Env(props=props) for _ in range(n)]
+    plain = orc.Env()
+    differs = False
+    for t in range(steps):
+        for i, e in enumerate(envs):
+            a = (np.float32(0.37) * np.float32((i + 3 * t + np.arange(4)) % 7) - np.float32(1.1)).astype(np.float32)
+            _, r, d = e.step(a)
+            if i == 0:
+                plain.step(a)
+    states = {int(l.split()[1]): np.array(l.split()[2:], np.float32) for l in out if l.startswith("S ")}
+    for i, e in enumerate(envs):
+        np.testing.assert_array_equal(states[i], e.obs())
+    differs = not np.array_equal(envs[0].obs(), plain.obs())
+    assert differs  # the box reached the walker
+
+
+@pytest.mark.gpu
 def test_mirror_saves_reference_weights_files(tmp_path, wk):
     """PPOAgent.Save (PPOAgent.cs:192-213): <FilePath>Data/Weights/{critic,actor}.weights"""
     exe = build_mirror(tmp_path, wk)
