@@ -57,6 +57,18 @@ DEV void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// [16 samples][RS] tile addressing, bank-conflict-free both ways (MI355X_MICROARCH §LDS):
+// column groups of 4 are XOR-swizzled by row bits 1..2.  A lane (n, g) stores an f4 at
+// [row n][cols c..c+3] (ds_write_b128: 8-lane groups, banks mod 32 -> the 8 rows of a group
+// land on 8 distinct 16-B slots); a lane (n, g) reads [row 4t + g][col 16i + n]
+// (ds_read_b32: 32-lane halves; the swizzle is uniform over a half, so RS = 80 keeps the two
+// rows of a half on opposite 16-bank halves).
+DEV int tw(int row, int col4) { return row * mf::RS + (col4 ^ (((row >> 1) & 3) << 2)); }
+DEV int tr(int row, int col) { return row * mf::RS + (col ^ (((row >> 1) & 3) << 2)); }
+// [16][16] tiles (SX, G3): columns XOR-swizzled by 2 (row >> 1), read as [row n][col 4t + g]
+// and [row 4t + g][col n] without conflicts; the f4 store of SX moves its group and swaps
+// its element pairs accordingly
+DEV int sx(int row, int col) { return row * 16 + (col ^ ((row >> 1) << 1)); }
 DEV f4 mfma(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 // sum over the 16 lanes of a DPP row (all lanes get the total)
 DEV float row_sum16(float v) {
@@ -70,7 +82,7 @@ DEV float row_sum16(float v) {
 __global__ __launch_bounds__(64 * mf::WAVES) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_ppo_grad_mfma(GradArgs ga) {
   using namespace mf;
-  extern __shared__ float lds[];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, g = lane >> 4;
 
@@ -161,13 +173,17 @@ void k_ppo_grad_mfma(GradArgs ga) {
     if (c + nw < nchunks) nxt = gather(c + nw);
     const bool valid = c * 16 + n < ga.samples;
     const float act = cur.act, lpo = cur.lpo, ret = cur.ret, adv = cur.adv;
-    *(f4*)(cb + C_SX + n * 16 + 4 * g) = cur.sv;
+    {
+      const int h = (n >> 1) << 1;
+      const f4 v = (h & 2) ? f4{cur.sv[2], cur.sv[3], cur.sv[0], cur.sv[1]} : cur.sv;
+      *(f4*)(cb + C_SX + n * 16 + ((4 * g) ^ (h & 12))) = v;
+    }
     wave_sync();
 
     // ---- layer 1, actor and critic ----
     float sB[3];
 #pragma unroll
-    for (int t = 0; t < 3; t++) sB[t] = cb[C_SX + n * 16 + 4 * t + g];
+    for (int t = 0; t < 3; t++) sB[t] = cb[C_SX + sx(n, 4 * t + g)];
     f4 z1[4], zc1[4], h1[4], hc1[4];
 #pragma unroll
     for (int Mt = 0; Mt < 4; Mt++) {
@@ -186,8 +202,8 @@ void k_ppo_grad_mfma(GradArgs ga) {
       }
       z1[Mt] = acc;
       zc1[Mt] = accc;
-      *(f4*)(cb + C_H1 + n * RS + 16 * Mt + 4 * g) = h1[Mt];
-      *(f4*)(cb + C_HC1 + n * RS + 16 * Mt + 4 * g) = hc1[Mt];
+      *(f4*)(cb + C_H1 + tw(n, 16 * Mt + 4 * g)) = h1[Mt];
+      *(f4*)(cb + C_HC1 + tw(n, 16 * Mt + 4 * g)) = hc1[Mt];
     }
     // ---- layer 2 (B operand = layer 1's D registers) ----
     f4 w2[4][4];
@@ -209,7 +225,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
         h2[Mt][r] = mf_lrelu(acc[r]);
       }
       z2[Mt] = acc;
-      *(f4*)(cb + C_H2 + n * RS + 16 * Mt + 4 * g) = h2[Mt];
+      *(f4*)(cb + C_H2 + tw(n, 16 * Mt + 4 * g)) = h2[Mt];
     }
     // ---- output rows: actor z3[0..3] on h2, critic V on hc1 ----
     float p3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, pv = 0.0f;
@@ -271,10 +287,10 @@ void k_ppo_grad_mfma(GradArgs ga) {
       diagA += use ? ((((0.0f + al[0]) + al[1]) + al[2]) + al[3]) / 4.0f : 0.0f;
       skipped += (valid && !use) ? 1.0f : 0.0f;
       dbc2 += criticLoss;
-      cb[C_G3 + n * 16 + 4] = criticLoss;
+      cb[C_G3 + sx(n, 4)] = criticLoss;
     }
     db3 += gz3;
-    cb[C_G3 + n * 16 + g] = gz3;
+    cb[C_G3 + sx(n, g)] = gz3;
     // ---- gh2 = W3^T gz3 -> gz2; critic gzc1 = (Wc2 dV) * lrelu'(zc1) ----
     f4 gz2[4], gzc1[4];
 #pragma unroll
@@ -289,7 +305,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
         const float ghc1 = 0.0f + wc2[Mt][r] * criticLoss;  // same in the sample's 4 lanes
         gzc1[Mt][r] = ghc1 * mf_dlrelu(zc1[Mt][r]);
       }
-      *(f4*)(cb + C_G2 + n * RS + 16 * Mt + 4 * g) = gz2[Mt];
+      *(f4*)(cb + C_G2 + tw(n, 16 * Mt + 4 * g)) = gz2[Mt];
     }
     wave_sync();
     // ---- dW3 | dWc2 += [gz3; dV]^T [H2 | Hc1]; dW2 += gz2^T H1 (samples on K) ----
@@ -298,16 +314,16 @@ void k_ppo_grad_mfma(GradArgs ga) {
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         const int s = 4 * t + g;
-        av[t] = cb[C_G3 + s * 16 + n];
+        av[t] = cb[C_G3 + sx(s, n)];
 #pragma unroll
         for (int Nt = 0; Nt < 4; Nt++) {
-          bv[t][Nt] = cb[C_H2 + s * RS + 16 * Nt + n];
-          bv[t][Nt + 4] = cb[C_HC1 + s * RS + 16 * Nt + n];
+          bv[t][Nt] = cb[C_H2 + tr(s, 16 * Nt + n)];
+          bv[t][Nt + 4] = cb[C_HC1 + tr(s, 16 * Nt + n)];
         }
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-          ag[t][i] = cb[C_G2 + s * RS + 16 * i + n];
-          bh[t][i] = cb[C_H1 + s * RS + 16 * i + n];
+          ag[t][i] = cb[C_G2 + tr(s, 16 * i + n)];
+          bh[t][i] = cb[C_H1 + tr(s, 16 * i + n)];
         }
       }
 #pragma unroll
@@ -336,8 +352,8 @@ void k_ppo_grad_mfma(GradArgs ga) {
       f4 gz1;
 #pragma unroll
       for (int r = 0; r < 4; r++) gz1[r] = acc[r] * mf_dlrelu(z1[Mk][r]);
-      *(f4*)(cb + C_G1 + n * RS + 16 * Mk + 4 * g) = gz1;
-      *(f4*)(cb + C_GC1 + n * RS + 16 * Mk + 4 * g) = gzc1[Mk];
+      *(f4*)(cb + C_G1 + tw(n, 16 * Mk + 4 * g)) = gz1;
+      *(f4*)(cb + C_GC1 + tw(n, 16 * Mk + 4 * g)) = gzc1[Mk];
     }
     wave_sync();
     // ---- dW1 | db1, dWc1 | dbc1 += gz1^T [S | 1] ----
@@ -346,11 +362,11 @@ void k_ppo_grad_mfma(GradArgs ga) {
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         const int s = 4 * t + g;
-        bx[t] = cb[C_SX + s * 16 + n];
+        bx[t] = cb[C_SX + sx(s, n)];
 #pragma unroll
         for (int Mj = 0; Mj < 4; Mj++) {
-          a1v[t][Mj] = cb[C_G1 + s * RS + 16 * Mj + n];
-          a1cv[t][Mj] = cb[C_GC1 + s * RS + 16 * Mj + n];
+          a1v[t][Mj] = cb[C_G1 + tr(s, 16 * Mj + n)];
+          a1cv[t][Mj] = cb[C_GC1 + tr(s, 16 * Mj + n)];
         }
       }
 #pragma unroll

@@ -1,7 +1,8 @@
 """Physics-kernel microbenchmark: rollout (policy fused) vs physics-only env-steps.
 
   python scripts/phys_bench.py [n_walkers] [T] [lanes...]
-Prints ms per launch and env-steps/s for each lane mapping.
+Prints ms per launch and env-steps/s for each lane mapping.  WK_SCENE=1: with the four scene
+props of tests/test_gpu_scene.py (scene_a; the one-lane scene kernel).
 """
 import os
 import sys
@@ -17,6 +18,10 @@ T = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 lanes = [int(x) for x in sys.argv[3:]] or [1, 2, 16]
 for L in lanes:
     eng = wk.Engine(n, seed=20250905, Horizon=T, RandomizeStart=1, LanesPerWalker=L)
+    if os.environ.get("WK_SCENE"):
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from test_gpu_scene import scene_a
+        eng.set_scene(scene_a(wk.make_prop))
     g = torch.Generator(device="cuda").manual_seed(1)
     act = torch.rand((T, n, 4), device="cuda", generator=g) * 2 - 1
     rew = torch.empty((T, n), device="cuda")
