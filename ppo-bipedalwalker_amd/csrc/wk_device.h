@@ -216,14 +216,20 @@ DEV void project2(float ax, float ay, const Poly<NA>& A, const Poly<NB>& B, floa
 // min over corners of fl(fl(ax x) + fl(ay y)) = fl(min_x fl(ax x) + min_y fl(ay y)) (and
 // likewise max): the box projects in 4 products, 2 min, 2 max, 2 adds instead of a
 // 4-vertex loop -- the same values (a zero's sign aside, which no overlapping axis sees).
-template <int NP, int NQ, bool FLOORQ = false>
+//
+// Verdict algebra (finite state; a non-finite state is already a fault): fl(a - b) > 0 iff
+// a > b, so the axis overlaps iff temp = min(qmax - pmin, pmax - qmin) > 0; and a depth or
+// normal is only ever used when no axis separates, so an axis may be taken on temp < depth
+// alone -- whenever a separating axis exists the caller discards both.  ZE: P may have a
+// zero edge (a rough-floor segment); a walker polygon's rigid edges never vanish.
+template <int NP, int NQ, bool FLOORQ = false, bool ZE = false>
 DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, float& depth) {
 #pragma unroll
   for (int i = 0; i < NP; i++) {
     const int i1 = (i + 1) % NP;
     const float ex = P.x[i1] - P.x[i], ey = P.y[i1] - P.y[i];
     V2 axis = mk(-ey, ex);
-    const bool valid = !(axis.x == 0.0f && axis.y == 0.0f);
+    const bool valid = !ZE || !(axis.x == 0.0f && axis.y == 0.0f);
     axis = vnormalize_edge(axis);  // garbage for a zero edge: masked by `valid`
     float pmin, pmax, qmin, qmax;
     if constexpr (FLOORQ) {
@@ -242,9 +248,8 @@ DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, 
       project2(axis.x, axis.y, P, Q, pmin, pmax, qmin, qmax);
     }
     const float temp = __builtin_fminf(qmax - pmin, pmax - qmin);
-    const bool overlapping = (pmin < qmax) && (qmin < pmax);
-    sep = sep || (valid && !overlapping);
-    const bool take = valid && overlapping && temp < depth;
+    sep = sep || (valid && !(temp > 0.0f));
+    const bool take = valid && temp < depth;
     depth = take ? temp : depth;
     normal.x = take ? axis.x : normal.x;
     normal.y = take ? axis.y : normal.y;
@@ -260,9 +265,8 @@ DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, 
 DEV void floor_axis(float pmin, float pmax, float qmin, float qmax, float nx, float ny, bool& sep,
                     V2& normal, float& depth) {
   const float temp = __builtin_fminf(qmax - pmin, pmax - qmin);
-  const bool overlapping = (pmin < qmax) && (qmin < pmax);
-  sep = sep || !overlapping;
-  const bool take = overlapping && temp < depth;
+  sep = sep || !(temp > 0.0f);
+  const bool take = temp < depth;  // see axis_pass
   depth = take ? temp : depth;
   normal.x = take ? nx : normal.x;
   normal.y = take ? ny : normal.y;
@@ -283,13 +287,13 @@ DEV bool sat_floor(const Poly<NA>& A, const Poly<4>& F, float mnx, float mny, fl
   return !sep;
 }
 
-template <int NA, int NB>
+template <int NA, int NB, bool BZE = false>
 DEV bool sat(const Poly<NA>& A, const Poly<NB>& B, V2& normal, float& depth) {
   normal = mk(0.0f, 0.0f);
   depth = FLT_MAX;
   bool sep = false;
-  axis_pass(A, B, sep, normal, depth);
-  axis_pass(B, A, sep, normal, depth);
+  axis_pass<NA, NB, false, false>(A, B, sep, normal, depth);
+  axis_pass<NB, NA, false, BZE>(B, A, sep, normal, depth);
   V2 dir = mk(B.cx - A.cx, B.cy - A.cy);
   if (vdot(dir, normal) > 0.0f) normal = vmul(normal, -1.0f);
   return !sep;

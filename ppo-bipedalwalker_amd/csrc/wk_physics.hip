@@ -236,7 +236,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   bool hit;
   if constexpr (L > 1) hit = sat_row<L>(A, B, sub, n, depth);
   else if constexpr (FLAT) hit = sat_floor(A, B, mnx, mny, mxx, mxy, n, depth);
-  else hit = sat(A, B, n, depth);
+  else hit = sat<NA, NB, GENERIC>(A, B, n, depth);
   rp_mark(rp, RP_SAT);
   DUP(2, { const auto Ap = perturbed(A); V2 n2; float d2;
            const bool h2 = sat(Ap, B, n2, d2); sink(n2.x); sink(n2.y); sink(d2); sink(h2 ? 1.0f : 0.0f); });
