@@ -1290,10 +1290,12 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
   CkptHeader h;
   if (data.size() < sizeof h) { SETERR(c, "checkpoint '%s' truncated", path); return WK_ERR_ARG; }
   memcpy(&h, data.data(), sizeof h);
-  size_t need = ckpt_bytes(n) + sizeof(int32_t);
+  // version 2 (before scene props) has no scene section; version 3 always has one
+  const bool v2 = h.version == 2;
+  size_t need = ckpt_bytes(n) + (v2 ? 0 : sizeof(int32_t));
   int32_t np = 0;
   std::vector<wk_prop> desc;
-  if (data.size() >= need) {
+  if (!v2 && data.size() >= need) {
     memcpy(&np, data.data() + need - sizeof(int32_t), sizeof np);
     if (np > 0 && np <= WK_MAX_PROPS && data.size() >= need + sizeof(wk_prop) * np) {
       desc.resize(np);
@@ -1308,7 +1310,7 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
       need += sizeof(float) * n * pstride;
     }
   }
-  if (h.magic != kCkptMagic || h.version != kCkptVersion) { SETERR(c, "'%s' is not a wk checkpoint", path); return WK_ERR_ARG; }
+  if (h.magic != kCkptMagic || (h.version != kCkptVersion && !v2)) { SETERR(c, "'%s' is not a wk checkpoint", path); return WK_ERR_ARG; }
   if (h.n_env != n || h.nstate != (uint32_t)wk::NSTATE || h.nparam != (uint32_t)wk::NPARAM || data.size() != need) {
     SETERR(c, "checkpoint '%s' is for %u walkers (context has %zu)", path, h.n_env, n);
     return WK_ERR_ARG;
@@ -1331,7 +1333,7 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
   HIPCHK(c, hipMemcpy(c->ep_len, q, sizeof(int32_t) * n, hipMemcpyHostToDevice)); q += sizeof(int32_t) * n;
   // the scene: rebuilt from its descriptions, then every walker's saved prop state
   if (int r = wk_set_scene(c, desc.data(), (int)desc.size()); r != WK_OK) return r;
-  if (np > 0) {
+  if (np > 0) {  // (np > 0 only in a version-3 file)
     q += sizeof(int32_t) + sizeof(wk_prop) * np;
     HIPCHK(c, hipMemcpy(c->props, q, sizeof(float) * n * c->scene.pstride, hipMemcpyHostToDevice));
   }

@@ -222,8 +222,12 @@ DEV void project2(float ax, float ay, const Poly<NA>& A, const Poly<NB>& B, floa
 // normal is only ever used when no axis separates, so an axis may be taken on temp < depth
 // alone -- whenever a separating axis exists the caller discards both.  ZE: P may have a
 // zero edge (a rough-floor segment); a walker polygon's rigid edges never vanish.
+//
+// AX (optional): the normalised axes, kept for the contact faces (see EdgeAxes).
+template <int N> struct EdgeAxes { float x[N], y[N]; };
 template <int NP, int NQ, bool FLOORQ = false, bool ZE = false>
-DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, float& depth) {
+DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, float& depth,
+                   EdgeAxes<NP>* AX = nullptr) {
 #pragma unroll
   for (int i = 0; i < NP; i++) {
     const int i1 = (i + 1) % NP;
@@ -231,6 +235,7 @@ DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, 
     V2 axis = mk(-ey, ex);
     const bool valid = !ZE || !(axis.x == 0.0f && axis.y == 0.0f);
     axis = vnormalize_edge(axis);  // garbage for a zero edge: masked by `valid`
+    if (AX) { AX->x[i] = axis.x; AX->y[i] = axis.y; }
     float pmin, pmax, qmin, qmax;
     if constexpr (FLOORQ) {
       pmin = FLT_MAX; pmax = -FLT_MAX;
@@ -273,11 +278,11 @@ DEV void floor_axis(float pmin, float pmax, float qmin, float qmax, float nx, fl
 }
 template <int NA>
 DEV bool sat_floor(const Poly<NA>& A, const Poly<4>& F, float mnx, float mny, float mxx,
-                   float mxy, V2& normal, float& depth) {
+                   float mxy, V2& normal, float& depth, EdgeAxes<NA>* AX = nullptr) {
   normal = mk(0.0f, 0.0f);
   depth = FLT_MAX;
   bool sep = false;
-  axis_pass<NA, 4, true>(A, F, sep, normal, depth);
+  axis_pass<NA, 4, true>(A, F, sep, normal, depth, AX);
   floor_axis(-50.0f, 1050.0f, mnx, mxx, 1.0f, 0.0f, sep, normal, depth);
   floor_axis(900.0f, 1050.0f, mny, mxy, -0.0f, 1.0f, sep, normal, depth);
   floor_axis(-1050.0f, 50.0f, -mxx, -mnx, -1.0f, 0.0f, sep, normal, depth);
@@ -288,12 +293,13 @@ DEV bool sat_floor(const Poly<NA>& A, const Poly<4>& F, float mnx, float mny, fl
 }
 
 template <int NA, int NB, bool BZE = false>
-DEV bool sat(const Poly<NA>& A, const Poly<NB>& B, V2& normal, float& depth) {
+DEV bool sat(const Poly<NA>& A, const Poly<NB>& B, V2& normal, float& depth,
+             EdgeAxes<NA>* AXA = nullptr, EdgeAxes<NB>* AXB = nullptr) {
   normal = mk(0.0f, 0.0f);
   depth = FLT_MAX;
   bool sep = false;
-  axis_pass<NA, NB, false, false>(A, B, sep, normal, depth);
-  axis_pass<NB, NA, false, BZE>(B, A, sep, normal, depth);
+  axis_pass<NA, NB, false, false>(A, B, sep, normal, depth, AXA);
+  axis_pass<NB, NA, false, BZE>(B, A, sep, normal, depth, AXB);
   V2 dir = mk(B.cx - A.cx, B.cy - A.cy);
   if (vdot(dir, normal) > 0.0f) normal = vmul(normal, -1.0f);
   return !sep;
@@ -441,6 +447,63 @@ DEV void significant_face(const Poly<N>& P, V2 n, V2& fa, V2& fb, V2& fmax) {
   fmax = sig;
 }
 
+// The same face from the SAT's normalised axes (no new normalisation).  Axis i of P is
+// vnormalize_edge((-ey, ex)) of edge e_i = v_{i+1} - v_i, i.e. (-ey val, ex val) with
+// val = 1 / |e_i| (the squared length sums the same two exact squares, so val is
+// Normalize's): e_i's Normalize is (axis.y, -axis.x) bit for bit, and a negated vector
+// normalises to the negated result.  So after = Normalize(v_i - v_{i+1}) = -ê_i and
+// before = Normalize(v_i - v_{i-1}) = ê_{i-1}; the face direction Normalize(fb - fa) is
+// -before (face [sig, prev]) or after (face [next, sig]), returned in fdir.  (With no
+// projection below MaxValue -- a NaN normal, already a fault -- the reference's Zero
+// vertex is not on an edge; the result then differs from the reference's NaNs only in value.)
+template <int N>
+DEV void significant_face_ax(const Poly<N>& P, const EdgeAxes<N>& AX, V2 n, V2& fa, V2& fb,
+                             V2& fmax, V2& fdir) {
+  float mind = FLT_MAX;
+  uint32_t sx = 0u, sy = 0u;
+  uint32_t ax = __float_as_uint(P.x[0]), ay = __float_as_uint(P.y[0]);
+  uint32_t bx = __float_as_uint(P.x[N - 2]), by = __float_as_uint(P.y[N - 2]);
+  uint32_t ex = __float_as_uint(AX.x[N - 1]), ey = __float_as_uint(AX.y[N - 1]);  // axis i
+  uint32_t px = __float_as_uint(AX.x[N - 2]), py = __float_as_uint(AX.y[N - 2]);  // axis i-1
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const float p = P.x[i] * n.x + P.y[i] * n.y;
+    const bool lt = p < mind;
+    const uint32_t m = lt ? 0xffffffffu : 0u;
+    mind = lt ? p : mind;
+    sx = bsel(m, P.x[i], sx);
+    sy = bsel(m, P.y[i], sy);
+    ax = bsel(m, P.x[(i + 1) % N], ax);
+    ay = bsel(m, P.y[(i + 1) % N], ay);
+    bx = bsel(m, P.x[(i + N - 1) % N], bx);
+    by = bsel(m, P.y[(i + N - 1) % N], by);
+    ex = bsel(m, AX.x[i], ex);
+    ey = bsel(m, AX.y[i], ey);
+    px = bsel(m, AX.x[(i + N - 1) % N], px);
+    py = bsel(m, AX.y[(i + N - 1) % N], py);
+  }
+  const V2 sig = mk(__uint_as_float(sx), __uint_as_float(sy));
+  const V2 va = mk(__uint_as_float(ax), __uint_as_float(ay));
+  const V2 vb = mk(__uint_as_float(bx), __uint_as_float(by));
+  const V2 after = mk(-__uint_as_float(ey), __uint_as_float(ex));    // -(axis_i.y, -axis_i.x)
+  const V2 before = mk(__uint_as_float(py), -__uint_as_float(px));  // (axis_{i-1}.y, -axis_{i-1}.x)
+  const bool first = vdot(n, before) >= vdot(n, after);
+  fa = first ? sig : va;
+  fb = first ? vb : sig;
+  fmax = sig;
+  fdir = first ? vneg(before) : after;
+}
+// the flat floor's normalised edges (Environment.cs:219-223): (0,-150), (1100,0), (0,150),
+// (-1100,0) normalise to exactly (+0,-1), (1,+0), (+0,1), (-1,+0); as axes (-ey, ex) * val
+DEV EdgeAxes<4> floor_axes() {
+  EdgeAxes<4> a;
+  a.x[0] = 1.0f;  a.y[0] = 0.0f;    // edge (+0,-1)
+  a.x[1] = -0.0f; a.y[1] = 1.0f;    // edge (1,+0)
+  a.x[2] = -1.0f; a.y[2] = 0.0f;    // edge (+0,1)
+  a.x[3] = -0.0f; a.y[3] = -1.0f;   // edge (-1,+0)
+  return a;
+}
+
 // ClipVectors (:56-76), branch-free: the kept points in order [a], [b], [crossing]
 DEV int clip_vectors(V2 a, V2 b, V2 n, float offset, V2& o0, V2& o1) {
   const float da = vdot(a, n) - offset;
@@ -456,6 +519,41 @@ DEV int clip_vectors(V2 a, V2 b, V2 n, float offset, V2& o0, V2& o1) {
   o0 = has0 ? r0 : o0;
   o1 = has1 ? r1 : o1;
   return (int)ka + (int)kb + (int)kx;
+}
+
+// GetContactPoints with both polygons' SAT axes kept: the faces' directions come normalised
+template <int NA, int NB>
+DEV int contact_points_ax(const Poly<NA>& A, const EdgeAxes<NA>& AXA, const Poly<NB>& B,
+                          const EdgeAxes<NB>& AXB, V2 normal, V2& c0, V2& c1) {
+  V2 ra, rb, rmax, rd, ia, ib, imax, id;
+  significant_face_ax(A, AXA, normal, ra, rb, rmax, rd);
+  V2 rf = vsub(rb, ra);
+  significant_face_ax(B, AXB, vneg(normal), ia, ib, imax, id);
+  V2 iv = vsub(ib, ia);
+  if (fabsf(vdot(rf, normal)) > fabsf(vdot(iv, normal))) {  // selects, not a branch
+    V2 t;
+    t = ra; ra = ia; ia = t;
+    t = rb; rb = ib; ib = t;
+    t = rmax; rmax = imax; imax = t;
+    rd = id;
+  }
+  rf = rd;  // Normalize(rb - ra)
+  float offset = vdot(rf, ra);
+  V2 p0 = mk(0.0f, 0.0f), p1 = mk(0.0f, 0.0f);
+  const int k1 = clip_vectors(ia, ib, rf, offset, p0, p1);
+  offset = vdot(rf, rb);
+  V2 q0 = mk(0.0f, 0.0f), q1 = mk(0.0f, 0.0f);
+  const int k2 = clip_vectors(p0, p1, vneg(rf), -offset, q0, q1);
+  if (k1 < 2 || k2 < 2) return 0;
+  V2 refn = mk(rf.y, -rf.x);
+  float maximum = vdot(refn, rmax);
+  int cnt = 2;
+  if (vdot(refn, q0) - maximum < 0.0f) { q0 = q1; cnt = 1; }
+  V2 last = cnt == 2 ? q1 : q0;
+  if (vdot(refn, last) - maximum < 0.0f) cnt = cnt == 2 ? 1 : 0;
+  c0 = q0;
+  c1 = q1;
+  return cnt;
 }
 
 template <int NA, int NB, bool SAFE = false>

@@ -234,15 +234,23 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   V2 n;
   float depth;
   bool hit;
+  // the one- and two-lane mappings keep both polygons' SAT axes for the contact faces
+  constexpr bool KEEP = L == 1 && !GENERIC;
+  EdgeAxes<NA> axa;
+  EdgeAxes<NB> axb;
   if constexpr (L > 1) hit = sat_row<L>(A, B, sub, n, depth);
-  else if constexpr (FLAT) hit = sat_floor(A, B, mnx, mny, mxx, mxy, n, depth);
+  else if constexpr (FLAT) hit = sat_floor(A, B, mnx, mny, mxx, mxy, n, depth, &axa);
+  else if constexpr (KEEP) hit = sat<NA, NB, false>(A, B, n, depth, &axa, &axb);
   else hit = sat<NA, NB, GENERIC>(A, B, n, depth);
   rp_mark(rp, RP_SAT);
   DUP(2, { const auto Ap = perturbed(A); V2 n2; float d2;
            const bool h2 = sat(Ap, B, n2, d2); sink(n2.x); sink(n2.y); sink(d2); sink(h2 ? 1.0f : 0.0f); });
   if (!hit) return;
   V2 c0, c1;
-  int nc = contact_points<NA, NB, GENERIC>(A, B, n, c0, c1);
+  int nc;
+  if constexpr (KEEP && FLAT) nc = contact_points_ax(A, axa, B, floor_axes(), n, c0, c1);
+  else if constexpr (KEEP) nc = contact_points_ax(A, axa, B, axb, n, c0, c1);
+  else nc = contact_points<NA, NB, GENERIC>(A, B, n, c0, c1);
   rp_mark(rp, RP_CONTACT);
   DUP(3, { const auto Ap = perturbed(A); V2 e0, e1;
            const int k2 = contact_points(Ap, B, n, e0, e1); sink(e0.x); sink(e1.y); sink((float)k2); });
@@ -294,7 +302,10 @@ DEV void joint_step(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, c
   V2 ab = vsub(mk(B.x[IB], B.y[IB]), mk(A.x[IA], A.y[IA]));
   float depth = vlen(ab);
   if (depth < 0.1f) return;
-  ab = vnormalize(ab);
+  // ab.Normalize(): ab * (1 / sqrt(x^2 + y^2)), and that sqrt is depth (same correctly
+  // rounded sqrt of the same sum); rcp_core is 1.0f / d bit for bit on [2^-48, 2^64]
+  const float rinv = depth <= 0x1p63f ? rcp_core(depth) : 1.0f / depth;
+  ab = mk(ab.x * rinv, ab.y * rinv);
   move(A, vdiv(vmul(ab, depth), 2.0f));
   move(B, vdiv(vmul(vneg(ab), depth), 2.0f));
   V2 contact = vdiv(vadd(mk(A.x[IA], A.y[IA]), mk(B.x[IB], B.y[IB])), 2.0f);

@@ -110,3 +110,25 @@ def test_checkpoint_mismatch_rejected(wk, tmp_path):
     with pytest.raises(wk.WkError, match="not a wk checkpoint"):
         a.checkpoint_load(tmp_path / "junk.ckpt")
     a.close()
+
+
+def test_checkpoint_version2_still_loads(wk, tmp_path):
+    """a version-2 file (no scene section: the layout before scene props) loads into a
+    context and clears its scene"""
+    import struct
+    a = wk.Engine(64, seed=SEED, RandomizeStart=1)
+    a.step(np.random.default_rng(1).uniform(-1, 1, (3, 64, 4)).astype(np.float32), k=3)
+    ck = tmp_path / "v3.ckpt"
+    a.checkpoint_save(ck)
+    raw = bytearray(ck.read_bytes())
+    assert struct.unpack_from("<I", raw, 4)[0] == 3 and raw[-4:] == b"\0\0\0\0"
+    struct.pack_into("<I", raw, 4, 2)
+    (tmp_path / "v2.ckpt").write_bytes(bytes(raw[:-4]))
+    b = wk.Engine(64, seed=SEED)
+    b.set_scene([wk.make_prop()])
+    b.checkpoint_load(tmp_path / "v2.ckpt")
+    np.testing.assert_array_equal(a.get_state(), b.get_state())
+    with pytest.raises(wk.WkError):
+        b.prop_view(0, 0)
+    a.close()
+    b.close()
