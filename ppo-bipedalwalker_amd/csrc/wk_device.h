@@ -23,20 +23,21 @@ DEV V2 vdiv(V2 a, float d) { float f = 1.0f / d; return mk(a.x * f, a.y * f); }
 DEV V2 vneg(V2 a) { return mk(-a.x, -a.y); }
 DEV float vdot(V2 a, V2 b) { return a.x * b.x + a.y * b.y; }
 // Correctly rounded sqrt / reciprocal without the library's rescaling and special-value
-// fixups.  For x >= 2^-96 HIP's sqrtf is v_sqrt_f32 plus a one-ulp round-to-nearest
-// correction (sqrt_core: the same ops); for a divisor in [2^-48, 2^64] the reciprocal
+// fixups.  For x in [2^-96, 2^126] HIP's sqrtf (v_sqrt_f32 plus a one-ulp round-to-nearest
+// correction) equals sqrt_core below; for a divisor in [2^-48, 2^64] the reciprocal
 // needs only v_rcp_f32 and one Newton step (rcp_core).  Both are checked bit for bit
 // against sqrtf and 1.0f/x over every non-negative float (tests/cpp/fastmath_check.hip).
 // Inputs outside [2^-96, 2^126] (never produced by walker-scale geometry) take the
 // library path.
+// On [2^-96, 2^126] the correctly rounded sqrt is also v_rsq_f32 y, s0 = x y and one FMA
+// correction s0 + (x - s0^2) (y / 2): 5 instructions instead of HIP's 9 (v_sqrt_f32 and
+// both neighbours' residuals).  Exhaustive: scripts/probe/sqrt_variants.hip, and the GPU
+// test's tests/cpp/fastmath_check.hip.
 DEV float sqrt_core(float x) {
-  float s = __builtin_amdgcn_sqrtf(x);
-  const float sd = __uint_as_float(__float_as_uint(s) - 1u);
-  const float su = __uint_as_float(__float_as_uint(s) + 1u);
-  const float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
-  s = (rd <= 0.0f) ? sd : s;
-  s = (ru > 0.0f) ? su : s;
-  return s;
+  const float y = __builtin_amdgcn_rsqf(x);
+  const float s0 = x * y;
+  const float e = __builtin_fmaf(-s0, s0, x);
+  return __builtin_fmaf(e, 0.5f * y, s0);
 }
 // v_rcp_f32 plus one Newton-Raphson step already equals the correctly rounded 1/d on
 // the whole domain (exhaustive: scripts/probe/fastmath_variants.hip, and the GPU test)
