@@ -163,3 +163,25 @@ def test_scene_validation(wk):
     side = wk.Engine(8, seed=SEED, LanesPerWalker=2)
     with pytest.raises(wk.WkError):
         side.set_scene([m()])
+
+
+def test_scene_at_bench_scale(wk, orc):
+    """65,536 walkers with the four props (the scene kernel at the bench's per-GPU size):
+    a strided sample of walkers replays bit-exactly through the oracle"""
+    n, k = 65536, 6
+    eng = wk.Engine(n, seed=SEED, RandomizeStart=1, RandomizeMaterial=1)
+    eng.set_scene(scene_a(wk.make_prop))
+    acts = np.random.default_rng(21).uniform(-1.2, 1.2, (k, n, 4)).astype(F)
+    obs, rew, done, fault = eng.step(acts, k=k)
+    sample = list(range(0, n, 1021))
+    envs = [orc.Env(dx=float(orc.env_offset(SEED, e)), material=int(orc.env_material(SEED, e)),
+                    props=scene_a(orc.make_prop)) for e in sample]
+    st = eng.get_state()
+    for i, e in zip(sample, envs):
+        for t in range(k):
+            o, r, d = e.step(acts[t, i])
+            assert r == rew[t, i] and d == done[t, i], (i, t)
+        np.testing.assert_array_equal(st[i], e.dump(), err_msg=f"walker {i}")
+        for p in range(4):
+            np.testing.assert_array_equal(eng.prop_view(i, p).vertex_array(), e.prop(p)[0])
+    assert not fault.any()
