@@ -9,11 +9,16 @@
 #include "wk_common.h"
 #include "wk_sincos_small.h"
 
+#ifndef WK_PACKED_PROJ
+#define WK_PACKED_PROJ 1
+#endif
+
 namespace wk {
 
 #define DEV __device__ __forceinline__
 
 struct V2 { float x, y; };
+typedef float pf2 __attribute__((ext_vector_type(2)));
 DEV V2 mk(float x, float y) { V2 r; r.x = x; r.y = y; return r; }
 DEV V2 vadd(V2 a, V2 b) { return mk(a.x + b.x, a.y + b.y); }
 DEV V2 vsub(V2 a, V2 b) { return mk(a.x - b.x, a.y - b.y); }
@@ -204,14 +209,39 @@ DEV void project2(float ax, float ay, const Poly<NA>& A, const Poly<NB>& B, floa
   }
 }
 
+// Projection of a polygon on an axis, min and max by value (see project2).  Vertex pairs go
+// through v_pk_mul_f32 / v_pk_add_f32: two IEEE fp32 products / sums per instruction, the
+// same per-element operations as ax * x + ay * y (no FMA: -ffp-contract=off).  Measured
+// -2 % rollout time; packing the rotation / move per (x, y) pair instead cost +25 % (register
+// shuffles), packing the contact-face projections changed nothing.
+template <int N>
+DEV void proj_minmax(const Poly<N>& P, float ax, float ay, float& mn, float& mx) {
+  float v[N];
+#if WK_PACKED_PROJ
+  const pf2 a2 = {ax, ax}, b2 = {ay, ay};
+#pragma unroll
+  for (int i = 0; i + 1 < N; i += 2) {
+    const pf2 q = (a2 * pf2{P.x[i], P.x[i + 1]}) + (b2 * pf2{P.y[i], P.y[i + 1]});
+    v[i] = q.x;
+    v[i + 1] = q.y;
+  }
+  if (N & 1) v[N - 1] = ax * P.x[N - 1] + ay * P.y[N - 1];
+#else
+#pragma unroll
+  for (int i = 0; i < N; i++) v[i] = ax * P.x[i] + ay * P.y[i];
+#endif
+  mn = FLT_MAX; mx = -FLT_MAX;
+#pragma unroll
+  for (int i = 0; i < N; i++) { mn = __builtin_fminf(mn, v[i]); mx = __builtin_fmaxf(mx, v[i]); }
+}
+
 // AxisChecks(vectorA = P's edges, vectorB = Q): projections of P then Q on each axis.
 // Branch-free: every axis is evaluated -- the loop's early `return false` only cuts
 // short a result whose normal / depth the caller discards -- a zero-length edge is
 // skipped by predication, and the first strict minimum wins exactly as in the loop.
 // (On an overlapping axis both differences are > 0, so Math.Min == v_min there.)
-// (Packed v_pk_mul/v_pk_add projections, two axes per instruction, measured 1.7x slower
-// on gfx950: each packed result needs a wait state before use and the pair costs two
-// passes anyway.  Scalar ops it is.)
+// (Packing two axes per instruction measured 1.7x slower -- each packed result needed a
+// wait state before use; two vertices per instruction, proj_minmax, is the packing kept.)
 // FLOORQ: Q is the flat floor box {x in (-50, 1050)} x {y in (900, 1050)}, all four
 // corner combinations.  Round-to-nearest addition is monotonic in each operand, so
 // min over corners of fl(fl(ax x) + fl(ay y)) = fl(min_x fl(ax x) + min_y fl(ay y)) (and
@@ -239,19 +269,14 @@ DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, 
     if (AX) { AX->x[i] = axis.x; AX->y[i] = axis.y; }
     float pmin, pmax, qmin, qmax;
     if constexpr (FLOORQ) {
-      pmin = FLT_MAX; pmax = -FLT_MAX;
-#pragma unroll
-      for (int k = 0; k < NP; k++) {
-        const float p = axis.x * P.x[k] + axis.y * P.y[k];
-        pmin = __builtin_fminf(pmin, p);
-        pmax = __builtin_fmaxf(pmax, p);
-      }
+      proj_minmax(P, axis.x, axis.y, pmin, pmax);
       const float x0 = axis.x * -50.0f, x1 = axis.x * 1050.0f;
       const float y0 = axis.y * 900.0f, y1 = axis.y * 1050.0f;
       qmin = __builtin_fminf(x0, x1) + __builtin_fminf(y0, y1);
       qmax = __builtin_fmaxf(x0, x1) + __builtin_fmaxf(y0, y1);
     } else {
-      project2(axis.x, axis.y, P, Q, pmin, pmax, qmin, qmax);
+      proj_minmax(P, axis.x, axis.y, pmin, pmax);
+      proj_minmax(Q, axis.x, axis.y, qmin, qmax);
     }
     const float temp = __builtin_fminf(qmax - pmin, pmax - qmin);
     sep = sep || (valid && !(temp > 0.0f));
