@@ -9,6 +9,9 @@
 #include "wk_common.h"
 #include "wk_sincos_small.h"
 
+#ifndef WK_PACKED_ROT
+#define WK_PACKED_ROT 1
+#endif
 #ifndef WK_PACKED_PROJ
 #define WK_PACKED_PROJ 1
 #endif
@@ -136,8 +139,18 @@ DEV void floor_poly(Poly<4>& f) {
 // Skeleton.Move (Skeleton.cs:76-85)
 template <int N>
 DEV void move(Poly<N>& p, V2 d) {
+#if WK_PACKED_ROT
+  const pf2 dx = {d.x, d.x}, dy = {d.y, d.y};
+#pragma unroll
+  for (int i = 0; i + 1 < N; i += 2) {
+    const pf2 x = pf2{p.x[i], p.x[i + 1]} + dx, y = pf2{p.y[i], p.y[i + 1]} + dy;
+    p.x[i] = x.x; p.x[i + 1] = x.y; p.y[i] = y.x; p.y[i + 1] = y.y;
+  }
+  if (N & 1) { p.x[N - 1] = p.x[N - 1] + d.x; p.y[N - 1] = p.y[N - 1] + d.y; }
+#else
 #pragma unroll
   for (int i = 0; i < N; i++) { p.x[i] = p.x[i] + d.x; p.y[i] = p.y[i] + d.y; }
+#endif
   p.cx = p.cx + d.x;
   p.cy = p.cy + d.y;
 }
@@ -154,6 +167,26 @@ DEV void rotate(Poly<N>& p, float angle) {
   else sincos((double)angle, &sd, &cd);
   const float c = (float)cd, s = (float)sd;
   const float m11 = c, m12 = s, m21 = -s, m22 = c;
+#if WK_PACKED_ROT
+  const pf2 cx = {p.cx, p.cx}, cy = {p.cy, p.cy}, z2 = {0.0f, 0.0f};
+  const pf2 a11 = {m11, m11}, a12 = {m12, m12}, a21 = {m21, m21}, a22 = {m22, m22};
+#pragma unroll
+  for (int i = 0; i + 1 < N; i += 2) {
+    const pf2 px = pf2{p.x[i], p.x[i + 1]} - cx, py = pf2{p.y[i], p.y[i + 1]} - cy;
+    const pf2 tx = ((px * a11) + (py * a21)) + z2;
+    const pf2 ty = ((px * a12) + (py * a22)) + z2;
+    const pf2 x = tx + cx, y = ty + cy;
+    p.x[i] = x.x; p.x[i + 1] = x.y; p.y[i] = y.x; p.y[i + 1] = y.y;
+  }
+  if (N & 1) {
+    const int i = N - 1;
+    float px = p.x[i] - p.cx, py = p.y[i] - p.cy;
+    float tx = (px * m11) + (py * m21) + 0.0f;
+    float ty = (px * m12) + (py * m22) + 0.0f;
+    p.x[i] = tx + p.cx;
+    p.y[i] = ty + p.cy;
+  }
+#else
 #pragma unroll
   for (int i = 0; i < N; i++) {
     float px = p.x[i] - p.cx, py = p.y[i] - p.cy;
@@ -162,6 +195,7 @@ DEV void rotate(Poly<N>& p, float angle) {
     p.x[i] = tx + p.cx;
     p.y[i] = ty + p.cy;
   }
+#endif
 }
 
 // BoundingBox.FindSignificantCorners + IsColliding (Skeleton.cs:133-176)
@@ -212,7 +246,8 @@ DEV void project2(float ax, float ay, const Poly<NA>& A, const Poly<NB>& B, floa
 // Projection of a polygon on an axis, min and max by value (see project2).  Vertex pairs go
 // through v_pk_mul_f32 / v_pk_add_f32: two IEEE fp32 products / sums per instruction, the
 // same per-element operations as ax * x + ay * y (no FMA: -ffp-contract=off).  Measured
-// -2 % rollout time; packing the rotation / move per (x, y) pair instead cost +25 % (register
+// (bench A/B on one box): -2 % rollout time; Skeleton.Move / Rotate over vertex pairs
+// (WK_PACKED_ROT) another -0.7 %; packing per (x, y) pair instead cost +25 % (register
 // shuffles), packing the contact-face projections changed nothing.
 template <int N>
 DEV void proj_minmax(const Poly<N>& P, float ax, float ay, float& mn, float& mx) {
