@@ -881,7 +881,9 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
     a.eps = k.AdamEpsilon;
   }
   float* part2 = c->partial + (size_t)nblocks * wk::SLAB;
-  const bool multi = c->comm && c->nranks > 1;
+  // with a communicator (any size, also one rank) the collective path runs: reduction,
+  // RCCL all-reduce, Adam -- a single-GPU test then covers the multi-GPU sequence
+  const bool multi = c->comm != nullptr;
   if (apply_adam && !multi) {  // one GPU: the last reduction stage applies Adam
     ProfScope ps(c, PK_REDUCE, 0, 2);
     HIPCHK(c, wk::launch_grad_reduce_adam(c->partial, nblocks, part2, c->grad, a, c->stream));

@@ -406,3 +406,26 @@ def test_baseline_config3_rollout_update_4096(wk, orc):
     eng.ppo_update(update_index=0)
     w1 = eng.get_weights()
     assert np.isfinite(w1).all() and not np.array_equal(w0, w1)
+
+
+def test_collective_path_matches_single_gpu_path(wk):
+    """The multi-GPU minibatch sequence (ordered reduction -> RCCL all-reduce -> Adam) run
+    through a one-rank communicator gives the same weights, Adam moments and diagnostics,
+    bit for bit, as the single-GPU fused reduction+Adam: the RCCL path of bench.py --gpus N
+    exercised on one device"""
+    n, T = 4096, 16
+    mk = lambda: wk.Engine(n, seed=SEED, Horizon=T, RandomizeStart=1, Minibatch=n // 4, Epochs=2)
+    a, b = mk(), mk()
+    b.comm_init(0, 1, wk.Engine.comm_unique_id())
+    out = []
+    for eng in (a, b):
+        eng.rollout(T)
+        d = eng.ppo_update(update_index=0)
+        eng.rollout(T)
+        d2 = eng.ppo_update(update_index=1)
+        out.append((eng.get_weights(), eng.get_adam(), d, d2))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    for x, y in zip(out[0][1], out[1][1]):
+        np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
+    assert out[0][2] == out[1][2] and out[0][3] == out[1][3]
+    np.testing.assert_array_equal(a.get_state(), b.get_state())
