@@ -8,7 +8,7 @@
  *   wk_create / wk_destroy     Environment ctor (Environment.cs:39-51), Walker ctor
  *                              (Walker/Walker.cs:25-46), PPOAgent ctor (PPOAgent.cs:23-37),
  *                              CreateFloor (Environment.cs:211-226)
- *   wk_step                    Environment.Update (Environment.cs:64-92): SampleActions
+ *   wk_step, wk_step_sampled   Environment.Update (Environment.cs:64-92): SampleActions
  *                              (PPOAgent.cs:381-398) or caller actions, Clip (:78),
  *                              Walker.TakeActions/Joint.SetTorque (Walker.cs:66-75,
  *                              Joint.cs:56-61), StepObjects (Environment.cs:126-143:
@@ -106,7 +106,7 @@ typedef struct wk_config {
   int LanesPerWalker;       /* physics kernel mapping (all bit-exact): 2 = a lane pair per
                                walker, left / right leg chains in parallel; 16 = SAT axes
                                over a 16-lane row; 1 = one walker per lane; 0 = auto
-                               (2 from 32,768 walkers, else 16) */
+                               (2 on the flat floor, 16 with RoughFloor) */
 } wk_config;
 
 /* The host-only fields of the reference's JSON configuration (SerializableHyperparameters,
@@ -242,6 +242,17 @@ int wk_set_offsets(wk_ctx* ctx, const float* dx /* n_env; start x = 125 + dx */)
 int wk_step(wk_ctx* ctx, const float* actions_or_null /* k*n_env*4, unclipped */, int k_steps,
             float* obs /* k*n_env*12 or NULL */, float* reward /* k*n_env or NULL */,
             uint8_t* done /* k*n_env or NULL */, uint32_t* fault /* n_env or NULL */);
+/* Environment.Update with the agent's own sampling, returning what Environment.cs:70-89
+ * records in the Trajectory: for each of k env-steps and walkers, the state observed before
+ * the step (_trajectory.States, :73), the sampled UNCLIPPED action (Walker.GetActions ->
+ * PPOAgent.SampleActions, :74 / PPOAgent.cs:381-398; recorded at :86), its per-dimension
+ * log-probability (:74, :87), the reward (:88) and terminal flag, the critic value of the
+ * state (GetValueEstimate, PPOAgent.cs:447-456) and the next state (post-reset after a
+ * terminal step).  Any output may be NULL.  Layouts [k][n_env][...]. */
+int wk_step_sampled(wk_ctx* ctx, int k_steps, float* states /* k*n*12 */,
+                    float* actions /* k*n*4 */, float* logp /* k*n*4 */,
+                    float* values /* k*n */, float* reward /* k*n */, uint8_t* done /* k*n */,
+                    float* next_obs /* k*n*12 */, uint32_t* fault /* n */);
 int wk_step_device(wk_ctx* ctx, const float* d_actions_or_null, int k_steps, float* d_obs,
                    float* d_reward, uint8_t* d_done, uint32_t* d_fault);
 /* one env-step with per-substep pair bookkeeping: trace[n_env * Iterations] */
@@ -361,6 +372,25 @@ int wk_allreduce_test(wk_ctx* ctx, float* host_buf, int n); /* sum in place (tes
 int wk_profile_enable(wk_ctx* ctx, int on);
 int wk_profile_get(wk_ctx* ctx, wk_profile* out);
 int wk_profile_reset(wk_ctx* ctx);
+
+/* Counting replay (the flop model priced on the physics events that actually
+ * happen, RigidBody.cs:66-96 / Joint.cs:31-41): steps the walkers k env-steps with the
+ * actions recorded in the device trajectory (rows 0..k-1 of the last rollout; k <= its
+ * horizon) through the one-lane kernel with per-lane event counters -- the same physics bit
+ * for bit as the rollout when the state is the rollout's starting state (see wk_snapshot).
+ * counts[WK_NEV] (added to, not cleared) receives, in order: joints past the 0.1 early-out;
+ * bounding-box hits leg-leg / leg-floor / torso-floor (each runs SAT); SAT collisions
+ * (contacts + MoveObjects) in the same three classes; contact resolutions with >= 1 point
+ * (the impulse pair) in the same three classes; contact points; walker-substeps; env-steps;
+ * auto-resets; 2 reserved. */
+#define WK_NEV 16
+int wk_count_events(wk_ctx* ctx, int k, uint64_t* counts);
+
+/* Device-side snapshot of the training state: walker records, Philox step counters, weights,
+ * Adam m / v / t, episode bookkeeping and scene props (not the trajectory buffer, which keeps
+ * the last rollout).  op 0 saves, op 1 restores (stream-ordered device copies, no host sync); bench.py restores one before every timed iteration so
+ * each measures the same regime (the throughput no longer drifts with training). */
+int wk_snapshot(wk_ctx* ctx, int op);
 
 #ifdef __cplusplus
 }

@@ -76,6 +76,11 @@ struct wk_ctx {
   std::vector<wk_prop> scene_desc;
   wk::SceneDev scene{};
   float* props = nullptr;
+  // wk_snapshot: one device block holding every snapshotted buffer, plus the host counters
+  void* snap = nullptr; size_t snap_bytes = 0;
+  int snap_adam_t = 0; uint32_t snap_rollout_steps = 0; uint64_t snap_loss_count = 0;
+  bool snap_valid = false;
+  unsigned long long* counts = nullptr;  // [WK_NEV] device (wk_count_events)
   // comm
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
@@ -87,6 +92,23 @@ struct wk_ctx {
   double prof_ms[PK_N] = {0};
   int64_t prof_cnt[PK_N] = {0};
   int64_t prof_units = 0;
+};
+
+// Every entry point binds the context's device for its duration: buffers are
+// allocated and copied on c->device whatever the calling thread's current device is, and the
+// caller's current device is restored afterwards.
+struct DevGuard {
+  int prev = -1;
+  bool switched = false;
+  explicit DevGuard(const wk_ctx* c) {
+    if (c && hipGetDevice(&prev) == hipSuccess && prev != c->device)
+      switched = hipSetDevice(c->device) == hipSuccess;
+  }
+  ~DevGuard() {
+    if (switched) (void)hipSetDevice(prev);
+  }
+  DevGuard(const DevGuard&) = delete;
+  DevGuard& operator=(const DevGuard&) = delete;
 };
 
 #define SETERR(ctx, ...)                                           \
@@ -249,6 +271,11 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
     return WK_ERR_HIP;
   }
   if (device < 0 || device >= ndev) { g_create_error = "device index out of range"; return WK_ERR_ARG; }
+  struct Restore {  // the caller's current device, as every other entry point leaves it
+    int prev = -1;
+    Restore() { if (hipGetDevice(&prev) != hipSuccess) prev = -1; }
+    ~Restore() { if (prev >= 0) (void)hipSetDevice(prev); }
+  } restore;
   wk_ctx* x = new wk_ctx();
   x->cfg = c;
   x->cfg.CriticNeuralNetwork = nullptr;
@@ -264,6 +291,9 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
     return code;
   };
   if (hipSetDevice(device) != hipSuccess) { x->err = "hipSetDevice failed"; return fail(WK_ERR_HIP); }
+  // > 64 KiB dynamic LDS for the gradient kernels, set on this device (the attribute is
+  // per device; wk_create is the only place, so launches never race on it)
+  if (wk::configure_device_kernels() != hipSuccess) { x->err = "hipFuncSetAttribute failed"; return fail(WK_ERR_HIP); }
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) {
     x->err = "hipStreamCreate failed";
     return fail(WK_ERR_HIP);
@@ -278,9 +308,12 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   P.std_ = expf(c.LogStandardDeviation);
   P.seed = seed;
   P.env_offset = c.EnvOffset;
-  // auto: the side-split pair mapping once it fills every SIMD twice (2 lanes x 32k
-  // walkers = 1024 SIMDs x 2 waves), the 16-lane SAT rows below that
-  P.lanes = c.LanesPerWalker ? c.LanesPerWalker : (c.RoughFloor || n_env < 32768 ? 16 : 2);
+  // auto: the side-split pair mapping on the flat floor at every size -- measured on one
+  // MI355X (scripts/probe_small.sh, rollout T = 64): 32.1 ms at 8,192 walkers vs 83.2 ms for
+  // the 16-lane rows and 104 ms one lane per walker; 32.9 vs 62.6 / 113 ms at 4,096.  Below
+  // 32,768 walkers the pair mapping leaves SIMDs idle, but a walker's substep chain on one
+  // wave still beats its 16-fold replication.  The rough floor runs on the 16-lane rows.
+  P.lanes = c.LanesPerWalker ? c.LanesPerWalker : (c.RoughFloor ? 16 : 2);
   P.rough = c.RoughFloor ? 1 : 0;
   const float PI_F = 3.14159265358979323846f;
   x->lp_const = -logf(P.std_) - logf(sqrtf(2.0f * PI_F));
@@ -351,6 +384,7 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
 }
 
 int wk_destroy(wk_ctx* c) {
+  DevGuard dg_(c);
   if (!c) return WK_OK;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& e : c->pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -359,7 +393,7 @@ int wk_destroy(wk_ctx* c) {
   void* bufs[] = {c->st, c->dxoff, c->mat, c->rng_t, c->W, c->Wz, c->m, c->v, c->grad, c->ts, c->ta,
                   c->tlp, c->tr, c->tv, c->tret, c->tadv, c->td, c->partial, c->scratch, c->scratch2,
                   c->ep_acc, c->ep_len, c->ep_scratch, c->ep_rowcnt, c->ep_count, c->ep_log,
-                  c->loss_log, c->props};
+                  c->loss_log, c->props, c->snap, c->counts};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -368,6 +402,7 @@ int wk_destroy(wk_ctx* c) {
 }
 
 int wk_sync(wk_ctx* c) {
+  DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return WK_OK;
@@ -376,6 +411,7 @@ int wk_sync(wk_ctx* c) {
 int wk_num_envs(const wk_ctx* c) { return c ? c->n : 0; }
 
 int wk_reset(wk_ctx* c, const uint8_t* mask) {
+  DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   const uint8_t* dmask = nullptr;
   if (mask) {
@@ -391,15 +427,20 @@ int wk_reset(wk_ctx* c, const uint8_t* mask) {
 }
 
 int wk_set_materials(wk_ctx* c, const int32_t* mat_id) {
+  DevGuard dg_(c);
   if (!c || !mat_id) return WK_ERR_ARG;
   for (int e = 0; e < c->n; e++)
     if (mat_id[e] < 0 || mat_id[e] > 7) { SETERR(c, "invalid material id %d at env %d", mat_id[e], e); return WK_ERR_ARG; }
+  // the context's stream is non-blocking: queued rollouts read mat (also on auto-reset)
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(c->mat, mat_id, sizeof(int32_t) * c->n, hipMemcpyHostToDevice));
   return WK_OK;
 }
 
 int wk_set_offsets(wk_ctx* c, const float* dx) {
+  DevGuard dg_(c);
   if (!c || !dx) return WK_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // queued kernels read dxoff on auto-reset
   HIPCHK(c, hipMemcpy(c->dxoff, dx, sizeof(float) * c->n, hipMemcpyHostToDevice));
   return WK_OK;
 }
@@ -430,12 +471,14 @@ static int step_impl(wk_ctx* c, const float* d_actions, int k, float* d_obs, flo
 
 int wk_step_device(wk_ctx* c, const float* d_actions, int k, float* d_obs, float* d_rew,
                    uint8_t* d_done, uint32_t* d_fault) {
+  DevGuard dg_(c);
   if (!c || k <= 0) return WK_ERR_ARG;
   return step_impl(c, d_actions, k, d_obs, d_rew, d_done, d_fault, d_actions ? 0 : 2, nullptr);
 }
 
 int wk_step(wk_ctx* c, const float* actions, int k, float* obs, float* reward, uint8_t* done,
             uint32_t* fault) {
+  DevGuard dg_(c);
   if (!c || k <= 0) return WK_ERR_ARG;
   const size_t n = c->n;
   const size_t b_act = actions ? sizeof(float) * 4 * n * k : 0;
@@ -462,7 +505,52 @@ int wk_step(wk_ctx* c, const float* actions, int k, float* obs, float* reward, u
   return WK_OK;
 }
 
+int wk_step_sampled(wk_ctx* c, int k, float* states, float* actions, float* logp, float* values,
+                    float* reward, uint8_t* done, float* next_obs, uint32_t* fault) {
+  DevGuard dg_(c);
+  if (!c || k <= 0) return WK_ERR_ARG;
+  const size_t n = c->n, kn = (size_t)k * n;
+  // the policy-sampling kernel with RECORD rows pointed at scratch (the device trajectory
+  // buffer of wk_rollout is not touched)
+  const size_t b12 = sizeof(float) * 12 * kn, b4 = sizeof(float) * 4 * kn, b1 = sizeof(float) * kn;
+  const size_t b_fault = sizeof(uint32_t) * n;
+  const size_t total = 2 * b12 + 2 * b4 + 2 * b1 + kn + b_fault + 8 * 64;
+  if (ensure(c, &c->scratch2, &c->scratch2_bytes, total)) return WK_ERR_HIP;
+  char* p = (char*)c->scratch2;
+  auto take = [&](size_t bytes) { char* r = p; p += (bytes + 63) & ~(size_t)63; return r; };
+  float* d_s = (float*)take(b12);
+  float* d_a = (float*)take(b4);
+  float* d_lp = (float*)take(b4);
+  float* d_v = (float*)take(b1);
+  float* d_r = (float*)take(b1);
+  float* d_o = (float*)take(b12);
+  uint32_t* d_f = (uint32_t*)take(b_fault);
+  uint8_t* d_d = (uint8_t*)take(kn);
+  HIPCHK(c, hipMemsetAsync(d_f, 0, b_fault, c->stream));
+  wk::StepArgs A{};
+  A.st = c->st; A.dxoff = c->dxoff; A.mat = c->mat; A.rng_t = c->rng_t;
+  A.obs_out = next_obs ? d_o : nullptr; A.fault_out = d_f;
+  A.W = c->W; A.Wz = c->Wz; A.lp_const = c->lp_const;
+  A.traj_s = d_s; A.traj_a = d_a; A.traj_lp = d_lp; A.traj_r = d_r; A.traj_d = d_d; A.traj_v = d_v;
+  A.t0 = 0; A.k_steps = k;
+  {
+    ProfScope ps(c, PK_PHYS, (int64_t)kn);
+    HIPCHK(c, launch_physics(c, 3, A));
+  }
+  if (states) HIPCHK(c, hipMemcpyAsync(states, d_s, b12, hipMemcpyDeviceToHost, c->stream));
+  if (actions) HIPCHK(c, hipMemcpyAsync(actions, d_a, b4, hipMemcpyDeviceToHost, c->stream));
+  if (logp) HIPCHK(c, hipMemcpyAsync(logp, d_lp, b4, hipMemcpyDeviceToHost, c->stream));
+  if (values) HIPCHK(c, hipMemcpyAsync(values, d_v, b1, hipMemcpyDeviceToHost, c->stream));
+  if (reward) HIPCHK(c, hipMemcpyAsync(reward, d_r, b1, hipMemcpyDeviceToHost, c->stream));
+  if (done) HIPCHK(c, hipMemcpyAsync(done, d_d, kn, hipMemcpyDeviceToHost, c->stream));
+  if (next_obs) HIPCHK(c, hipMemcpyAsync(next_obs, d_o, b12, hipMemcpyDeviceToHost, c->stream));
+  if (fault) HIPCHK(c, hipMemcpyAsync(fault, d_f, b_fault, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return WK_OK;
+}
+
 int wk_step_traced(wk_ctx* c, const float* actions, wk_pair_trace* trace) {
+  DevGuard dg_(c);
   if (!c || !actions || !trace) return WK_ERR_ARG;
   static_assert(sizeof(wk_pair_trace) == sizeof(wk::PairTraceDev), "trace layout");
   const size_t n = c->n;
@@ -481,6 +569,7 @@ int wk_step_traced(wk_ctx* c, const float* actions, wk_pair_trace* trace) {
 }
 
 int wk_get_obs(wk_ctx* c, float* obs) {
+  DevGuard dg_(c);
   if (!c || !obs) return WK_ERR_ARG;
   if (ensure(c, &c->scratch, &c->scratch_bytes, sizeof(float) * 12 * c->n)) return WK_ERR_HIP;
   HIPCHK(c, wk::launch_get_obs(c->P, c->st, (float*)c->scratch, c->stream));
@@ -492,6 +581,7 @@ int wk_get_obs(wk_ctx* c, float* obs) {
 // the device state is [n_env][WK_STATE_FLOATS] (one 448-B record per walker), the same
 // layout as the canonical dump, so these are plain copies
 int wk_get_state(wk_ctx* c, float* state) {
+  DevGuard dg_(c);
   if (!c || !state) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(state, c->st, sizeof(float) * wk::NSTATE * c->n, hipMemcpyDeviceToHost));
@@ -499,6 +589,7 @@ int wk_get_state(wk_ctx* c, float* state) {
 }
 
 int wk_set_state(wk_ctx* c, const float* state) {
+  DevGuard dg_(c);
   if (!c || !state) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(c->st, state, sizeof(float) * wk::NSTATE * c->n, hipMemcpyHostToDevice));
@@ -506,6 +597,7 @@ int wk_set_state(wk_ctx* c, const float* state) {
 }
 
 int wk_get_body_view(wk_ctx* c, int env, int body, wk_body_view* o) {
+  DevGuard dg_(c);
   if (!c || !o || env < 0 || env >= c->n || body < 0 || body >= (c->P.rough ? 15 : 6)) return WK_ERR_ARG;
   memset(o, 0, sizeof(*o));
   if (c->P.rough && body >= 5) {  // rough-floor segment body - 5 (Environment.cs:230-261)
@@ -594,6 +686,7 @@ static const float kMatProps[8][3] = {  // Materials/*.cs: inverse mass, restitu
     {20.0f, 0.3f, 0.01f}, {1.0f, 0.3f, 0.1f}, {0.01f, 0.1f, 0.2f}, {11.0f, 1.0f, 1.0f}};
 
 int wk_set_scene(wk_ctx* c, const wk_prop* props, int n_props) {
+  DevGuard dg_(c);
   if (!c || n_props < 0 || (n_props > 0 && !props)) return WK_ERR_ARG;
   if (n_props > WK_MAX_PROPS) { SETERR(c, "at most %d scene props", (int)WK_MAX_PROPS); return WK_ERR_ARG; }
   if (n_props > 0 && c->P.rough) { SETERR(c, "scene props run with the flat floor (RoughFloor = 0)"); return WK_ERR_CONFIG; }
@@ -660,11 +753,13 @@ int wk_set_scene(wk_ctx* c, const wk_prop* props, int n_props) {
   if (c->props) (void)hipFree(c->props);
   c->props = dev;
   c->scene = S;
+  c->snap_valid = false;  // the snapshot's layout no longer matches
   c->scene_desc.assign(props, props + n_props);
   return WK_OK;
 }
 
 int wk_get_prop_view(wk_ctx* c, int env, int k, wk_prop_view* o) {
+  DevGuard dg_(c);
   if (!c || !o || env < 0 || env >= c->n || k < 0 || k >= c->scene.n_props) return WK_ERR_ARG;
   memset(o, 0, sizeof(*o));
   const int nv = c->scene.nv[k];
@@ -683,12 +778,14 @@ int wk_get_prop_view(wk_ctx* c, int env, int k, wk_prop_view* o) {
 }
 
 int wk_get_weights(wk_ctx* c, float* p) {
+  DevGuard dg_(c);
   if (!c || !p) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(p, c->W, sizeof(float) * wk::NPARAM, hipMemcpyDeviceToHost));
   return WK_OK;
 }
 int wk_set_weights(wk_ctx* c, const float* p) {
+  DevGuard dg_(c);
   if (!c || !p) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(c->W, p, sizeof(float) * wk::NPARAM, hipMemcpyHostToDevice));
@@ -697,6 +794,7 @@ int wk_set_weights(wk_ctx* c, const float* p) {
   return WK_OK;
 }
 int wk_get_adam(wk_ctx* c, float* m, float* v, int* t) {
+  DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (m) HIPCHK(c, hipMemcpy(m, c->m, sizeof(float) * wk::NPARAM, hipMemcpyDeviceToHost));
@@ -705,6 +803,7 @@ int wk_get_adam(wk_ctx* c, float* m, float* v, int* t) {
   return WK_OK;
 }
 int wk_set_adam(wk_ctx* c, const float* m, const float* v, int t) {
+  DevGuard dg_(c);
   if (!c || t < 0) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (m) HIPCHK(c, hipMemcpy(c->m, m, sizeof(float) * wk::NPARAM, hipMemcpyHostToDevice));
@@ -745,11 +844,13 @@ static int policy_impl(wk_ctx* c, int n, const float* obs, const int32_t* ids, c
 
 int wk_policy_sample(wk_ctx* c, int n, const float* obs, const int32_t* env_ids,
                      const uint32_t* steps, float* mean, float* act, float* logp) {
+  DevGuard dg_(c);
   if (!c || n <= 0 || !obs) return WK_ERR_ARG;
   return policy_impl(c, n, obs, env_ids, steps, mean, act, logp, nullptr);
 }
 
 int wk_value(wk_ctx* c, int n, const float* obs, float* v) {
+  DevGuard dg_(c);
   if (!c || n <= 0 || !obs || !v) return WK_ERR_ARG;
   return policy_impl(c, n, obs, nullptr, nullptr, nullptr, nullptr, nullptr, v);
 }
@@ -767,6 +868,7 @@ static int returns_impl(wk_ctx* c) {
 }
 
 int wk_rollout(wk_ctx* c, int horizon) {
+  DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   if (horizon <= 0) horizon = c->T;
   if (horizon > c->T) { SETERR(c, "horizon %d exceeds the configured Horizon %d", horizon, c->T); return WK_ERR_ARG; }
@@ -792,12 +894,14 @@ int wk_rollout(wk_ctx* c, int horizon) {
 }
 
 int wk_compute_returns(wk_ctx* c) {
+  DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   if (c->T_valid <= 0) { SETERR(c, "no trajectory recorded"); return WK_ERR_STATE; }
   return returns_impl(c);
 }
 
 int wk_rollout_stats_get(wk_ctx* c, wk_rollout_stats* o) {
+  DevGuard dg_(c);
   if (!c || !o) return WK_ERR_ARG;
   memset(o, 0, sizeof(*o));
   const size_t cnt = (size_t)c->n * c->T_valid;
@@ -815,6 +919,7 @@ int wk_rollout_stats_get(wk_ctx* c, wk_rollout_stats* o) {
 
 int wk_get_trajectory(wk_ctx* c, float* s, float* a, float* lp, float* r, uint8_t* d, float* v,
                       float* ret, float* adv) {
+  DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   const size_t cnt = (size_t)c->n * c->T_valid;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -831,6 +936,7 @@ int wk_get_trajectory(wk_ctx* c, float* s, float* a, float* lp, float* r, uint8_
 
 int wk_set_trajectory(wk_ctx* c, int horizon, const float* s, const float* a, const float* lp,
                       const float* r, const uint8_t* d, const float* v) {
+  DevGuard dg_(c);
   if (!c || horizon <= 0 || horizon > c->T || !s || !a || !lp || !r || !d || !v) return WK_ERR_ARG;
   const size_t cnt = (size_t)c->n * horizon;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -919,6 +1025,7 @@ static wk::GradArgs grad_base(wk_ctx* c) {
 
 static int ppo_update_impl(wk_ctx* c, const wk_ppo_args* args);
 int wk_ppo_update(wk_ctx* c, const wk_ppo_args* args, float* critic_diag, float* actor_diag) {
+  DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   if (c->T_valid <= 0) { SETERR(c, "wk_ppo_update before wk_rollout / wk_set_trajectory"); return WK_ERR_STATE; }
   {
@@ -1015,12 +1122,14 @@ static int batch_impl(wk_ctx* c, int wpb, int B, float b_div, const float* s, co
 int wk_train_batch(wk_ctx* c, int B, float b_div, const float* s, const float* a, const float* lpo,
                    const float* ret, const float* adv, float* cd, float* ad, float* grads_out,
                    int apply_adam, int* skipped) {
+  DevGuard dg_(c);
   return batch_impl(c, 1, B, b_div, s, a, lpo, ret, adv, cd, ad, grads_out, apply_adam, skipped);
 }
 
 int wk_minibatch_gradient(wk_ctx* c, int B, float b_div, const float* s, const float* a,
                           const float* lpo, const float* ret, const float* adv, float* cd,
                           float* ad, float* grads_out, int* skipped) {
+  DevGuard dg_(c);
   return batch_impl(c, 0, B, b_div, s, a, lpo, ret, adv, cd, ad, grads_out, 0, skipped);
 }
 
@@ -1035,6 +1144,7 @@ int wk_comm_unique_id(uint8_t* id) {
 }
 
 int wk_comm_init(wk_ctx* c, int rank, int nranks, const uint8_t* id) {
+  DevGuard dg_(c);
   if (!c || !id || nranks <= 0 || rank < 0 || rank >= nranks) return WK_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   ncclUniqueId u;
@@ -1047,6 +1157,7 @@ int wk_comm_init(wk_ctx* c, int rank, int nranks, const uint8_t* id) {
 }
 
 int wk_allreduce_test(wk_ctx* c, float* host_buf, int n) {
+  DevGuard dg_(c);
   if (!c || !host_buf || n <= 0) return WK_ERR_ARG;
   if (ensure(c, &c->scratch, &c->scratch_bytes, sizeof(float) * n)) return WK_ERR_HIP;
   HIPCHK(c, hipMemcpyAsync(c->scratch, host_buf, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
@@ -1059,13 +1170,81 @@ int wk_allreduce_test(wk_ctx* c, float* host_buf, int n) {
   return WK_OK;
 }
 
+int wk_count_events(wk_ctx* c, int k, uint64_t* counts) {
+  DevGuard dg_(c);
+  if (!c || !counts || k <= 0) return WK_ERR_ARG;
+  if (k > c->T_valid) { SETERR(c, "count replay of %d env-steps, the trajectory holds %d", k, c->T_valid); return WK_ERR_STATE; }
+  if (c->P.rough || c->scene.n_props > 0) { SETERR(c, "the counting replay runs on the flat floor without props"); return WK_ERR_CONFIG; }
+  static_assert(WK_NEV == wk::NEV, "event counters");
+  if (!c->counts) HIPCHK(c, hipMalloc((void**)&c->counts, sizeof(unsigned long long) * wk::NEV));
+  HIPCHK(c, hipMemsetAsync(c->counts, 0, sizeof(unsigned long long) * wk::NEV, c->stream));
+  wk::StepArgs A{};
+  A.st = c->st; A.dxoff = c->dxoff; A.mat = c->mat; A.rng_t = c->rng_t;
+  A.actions = c->ta; A.k_steps = k; A.counts = c->counts;
+  HIPCHK(c, wk::launch_env_step(4, c->P, A, c->stream));
+  unsigned long long h[wk::NEV];
+  HIPCHK(c, hipMemcpyAsync(h, c->counts, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int i = 0; i < wk::NEV; i++) counts[i] += (uint64_t)h[i];
+  return WK_OK;
+}
+
+int wk_snapshot(wk_ctx* c, int op) {
+  DevGuard dg_(c);
+  if (!c || op < 0 || op > 1) return WK_ERR_ARG;
+  const size_t n = c->n;
+  struct Seg { void* p; size_t bytes; };
+  const Seg segs[] = {
+      {c->st, sizeof(float) * wk::NSTATE * n}, {c->rng_t, sizeof(uint32_t) * n},
+      {c->W, sizeof(float) * wk::NPARAM}, {c->Wz, sizeof(float) * wk::mfma_image_floats()},
+      {c->m, sizeof(float) * wk::NPARAM}, {c->v, sizeof(float) * wk::NPARAM},
+      {c->ep_acc, sizeof(double) * n}, {c->ep_len, sizeof(int32_t) * n},
+      {c->ep_count, sizeof(uint64_t)},
+      {c->props, c->props ? sizeof(float) * n * c->scene.pstride : 0}};
+  size_t total = 0;
+  for (const Seg& g : segs) total += (g.bytes + 255) & ~(size_t)255;
+  if (op == 0) {
+    if (c->snap_bytes < total) {
+      if (c->snap) (void)hipFree(c->snap);
+      c->snap = nullptr; c->snap_bytes = 0;
+      HIPCHK(c, hipMalloc(&c->snap, total));
+      c->snap_bytes = total;
+    }
+    c->snap_adam_t = c->adam_t;
+    c->snap_rollout_steps = c->rollout_steps;
+    c->snap_loss_count = c->loss_count;
+  } else if (!c->snap_valid || c->snap_bytes < total) {
+    SETERR(c, "no snapshot of this configuration to restore");
+    return WK_ERR_STATE;
+  }
+  char* q = (char*)c->snap;
+  for (const Seg& g : segs) {
+    if (g.bytes)
+      HIPCHK(c, hipMemcpyAsync(op == 0 ? (void*)q : g.p, op == 0 ? g.p : (const void*)q, g.bytes,
+                               hipMemcpyDeviceToDevice, c->stream));
+    q += (g.bytes + 255) & ~(size_t)255;
+  }
+  if (op == 0) {
+    c->snap_valid = true;
+  } else {
+    c->adam_t = c->snap_adam_t;
+    c->rollout_steps = c->snap_rollout_steps;
+    c->loss_count = c->snap_loss_count;
+    // the trajectory buffer is not part of the snapshot: it keeps the last rollout (the
+    // counting replay reads its actions after a restore)
+  }
+  return WK_OK;
+}
+
 int wk_profile_enable(wk_ctx* c, int on) {
+  DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   c->prof = on < 0 ? 0 : (on > 2 ? 2 : on);
   return WK_OK;
 }
 
 int wk_profile_reset(wk_ctx* c) {
+  DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   prof_drain(c);
@@ -1075,6 +1254,7 @@ int wk_profile_reset(wk_ctx* c) {
 }
 
 int wk_profile_get(wk_ctx* c, wk_profile* o) {
+  DevGuard dg_(c);
   if (!c || !o) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   prof_drain(c);
@@ -1190,7 +1370,14 @@ struct CkptHeader {
   uint32_t rollout_steps;
 };
 static_assert(sizeof(CkptHeader) == 48, "checkpoint header");
-const uint32_t kCkptVersion = 3;  // 3: + scene section (int32 n_props, wk_prop[n_props], [n][pstride])
+// version 4 adds this block right after the header: the configuration that changes the
+// physics beyond the header's fields (RoughFloor) and the mapping the file was written with
+struct CkptExt {
+  int32_t rough_floor, lanes_per_walker, reserved0, reserved1;
+};
+static_assert(sizeof(CkptExt) == 16, "checkpoint extension");
+// 3: + scene section (int32 n_props, wk_prop[n_props], [n][pstride]); 4: + CkptExt
+const uint32_t kCkptVersion = 4;
 size_t ckpt_bytes(size_t n) {
   return sizeof(CkptHeader) + sizeof(float) * (3 * wk::NPARAM + n * wk::NSTATE + 2 * n) +
          sizeof(int32_t) * n + sizeof(double) * n + sizeof(int32_t) * n;
@@ -1223,6 +1410,7 @@ int wk_parse_weights(const char* critic, const char* actor, float* params) {
 }
 
 int wk_save_weights(wk_ctx* c, const char* critic_path, const char* actor_path) {
+  DevGuard dg_(c);
   if (!c || !critic_path || !actor_path) return WK_ERR_ARG;
   std::vector<float> p(wk::NPARAM);
   int r = wk_get_weights(c, p.data());
@@ -1237,6 +1425,7 @@ int wk_save_weights(wk_ctx* c, const char* critic_path, const char* actor_path) 
 }
 
 int wk_load_weights(wk_ctx* c, const char* critic_path, const char* actor_path) {
+  DevGuard dg_(c);
   if (!c || !critic_path || !actor_path) return WK_ERR_ARG;
   std::string ct, at;
   if (!read_file(critic_path, ct) || !read_file(actor_path, at)) {
@@ -1254,6 +1443,7 @@ int wk_load_weights(wk_ctx* c, const char* critic_path, const char* actor_path) 
 // Binary checkpoint for exact resume: weights, Adam m / v / t, every walker record,
 // Philox step counters, start offsets and materials.
 int wk_checkpoint_save(wk_ctx* c, const char* path) {
+  DevGuard dg_(c);
   if (!c || !path) return WK_ERR_ARG;
   const size_t n = c->n;
   CkptHeader h{kCkptMagic, kCkptVersion, (uint32_t)n, (uint32_t)wk::NSTATE, (uint32_t)wk::NPARAM,
@@ -1261,9 +1451,11 @@ int wk_checkpoint_save(wk_ctx* c, const char* path) {
                c->cfg.MaxTimesteps, c->rollout_steps};
   const int np = c->scene.n_props;
   const size_t scene_bytes = sizeof(int32_t) + sizeof(wk_prop) * np + sizeof(float) * n * c->scene.pstride;
-  std::vector<char> buf(ckpt_bytes(n) + scene_bytes);
+  const CkptExt ext{c->cfg.RoughFloor, c->P.lanes, 0, 0};
+  std::vector<char> buf(ckpt_bytes(n) + sizeof ext + scene_bytes);
   char* q = buf.data();
   memcpy(q, &h, sizeof h); q += sizeof h;
+  memcpy(q, &ext, sizeof ext); q += sizeof ext;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(q, c->W, sizeof(float) * wk::NPARAM, hipMemcpyDeviceToHost)); q += sizeof(float) * wk::NPARAM;
   HIPCHK(c, hipMemcpy(q, c->m, sizeof(float) * wk::NPARAM, hipMemcpyDeviceToHost)); q += sizeof(float) * wk::NPARAM;
@@ -1284,7 +1476,11 @@ int wk_checkpoint_save(wk_ctx* c, const char* path) {
   return WK_OK;
 }
 
+// Every check runs before the first device write, so a rejected file leaves the context
+// exactly as it was: header, sizes, seed / EnvOffset (the Philox streams),
+// Iterations / MaxTimesteps / RoughFloor (the physics), and the scene's acceptability.
 int wk_checkpoint_load(wk_ctx* c, const char* path) {
+  DevGuard dg_(c);
   if (!c || !path) return WK_ERR_ARG;
   std::string data;
   if (!read_file(path, data)) { SETERR(c, "cannot read checkpoint '%s'", path); return WK_ERR_ARG; }
@@ -1292,14 +1488,22 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
   CkptHeader h;
   if (data.size() < sizeof h) { SETERR(c, "checkpoint '%s' truncated", path); return WK_ERR_ARG; }
   memcpy(&h, data.data(), sizeof h);
-  // version 2 (before scene props) has no scene section; version 3 always has one
+  if (h.magic != kCkptMagic || h.version < 2 || h.version > kCkptVersion) {
+    SETERR(c, "'%s' is not a wk checkpoint", path);
+    return WK_ERR_ARG;
+  }
+  // version 2 (before scene props) has no scene section, version 3 no CkptExt
   const bool v2 = h.version == 2;
-  size_t need = ckpt_bytes(n) + (v2 ? 0 : sizeof(int32_t));
+  const size_t ext_bytes = h.version >= 4 ? sizeof(CkptExt) : 0;
+  CkptExt ext{0, 0, 0, 0};  // files before version 4 were flat-floor runs
+  if (ext_bytes && data.size() >= sizeof h + ext_bytes) memcpy(&ext, data.data() + sizeof h, sizeof ext);
+  size_t need = ckpt_bytes(n) + ext_bytes + (v2 ? 0 : sizeof(int32_t));
   int32_t np = 0;
   std::vector<wk_prop> desc;
   if (!v2 && data.size() >= need) {
     memcpy(&np, data.data() + need - sizeof(int32_t), sizeof np);
-    if (np > 0 && np <= WK_MAX_PROPS && data.size() >= need + sizeof(wk_prop) * np) {
+    if (np < 0 || np > WK_MAX_PROPS) { SETERR(c, "checkpoint '%s': invalid scene section", path); return WK_ERR_ARG; }
+    if (np > 0 && data.size() >= need + sizeof(wk_prop) * np) {
       desc.resize(np);
       memcpy(desc.data(), data.data() + need, sizeof(wk_prop) * np);
       need += sizeof(wk_prop) * np;
@@ -1312,7 +1516,6 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
       need += sizeof(float) * n * pstride;
     }
   }
-  if (h.magic != kCkptMagic || (h.version != kCkptVersion && !v2)) { SETERR(c, "'%s' is not a wk checkpoint", path); return WK_ERR_ARG; }
   if (h.n_env != n || h.nstate != (uint32_t)wk::NSTATE || h.nparam != (uint32_t)wk::NPARAM || data.size() != need) {
     SETERR(c, "checkpoint '%s' is for %u walkers (context has %zu)", path, h.n_env, n);
     return WK_ERR_ARG;
@@ -1322,7 +1525,22 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
            path, (unsigned long long)h.seed, h.env_offset, (unsigned long long)c->seed, c->cfg.EnvOffset);
     return WK_ERR_CONFIG;
   }
-  const char* q = data.data() + sizeof h;
+  if (h.iterations != c->cfg.Iterations || h.max_timesteps != c->cfg.MaxTimesteps ||
+      ext.rough_floor != c->cfg.RoughFloor) {
+    SETERR(c, "checkpoint '%s' was written with Iterations %d / MaxTimesteps %d / RoughFloor %d "
+              "(context: %d / %d / %d)", path, h.iterations, h.max_timesteps, ext.rough_floor,
+           c->cfg.Iterations, c->cfg.MaxTimesteps, c->cfg.RoughFloor);
+    return WK_ERR_CONFIG;
+  }
+  if (np > 0 && (c->P.rough || c->cfg.LanesPerWalker > 1)) {  // wk_set_scene would refuse it
+    SETERR(c, "checkpoint '%s' has scene props, which need the flat floor and the one-lane "
+              "mapping (LanesPerWalker 0 or 1)", path);
+    return WK_ERR_CONFIG;
+  }
+  // the scene first: wk_set_scene is all-or-nothing and is the last step that can fail on
+  // anything but a device error
+  if (int r = wk_set_scene(c, desc.data(), (int)desc.size()); r != WK_OK) return r;
+  const char* q = data.data() + sizeof h + ext_bytes;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(c->W, q, sizeof(float) * wk::NPARAM, hipMemcpyHostToDevice)); q += sizeof(float) * wk::NPARAM;
   HIPCHK(c, hipMemcpy(c->m, q, sizeof(float) * wk::NPARAM, hipMemcpyHostToDevice)); q += sizeof(float) * wk::NPARAM;
@@ -1333,9 +1551,7 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
   HIPCHK(c, hipMemcpy(c->mat, q, sizeof(int32_t) * n, hipMemcpyHostToDevice)); q += sizeof(int32_t) * n;
   HIPCHK(c, hipMemcpy(c->ep_acc, q, sizeof(double) * n, hipMemcpyHostToDevice)); q += sizeof(double) * n;
   HIPCHK(c, hipMemcpy(c->ep_len, q, sizeof(int32_t) * n, hipMemcpyHostToDevice)); q += sizeof(int32_t) * n;
-  // the scene: rebuilt from its descriptions, then every walker's saved prop state
-  if (int r = wk_set_scene(c, desc.data(), (int)desc.size()); r != WK_OK) return r;
-  if (np > 0) {  // (np > 0 only in a version-3 file)
+  if (np > 0) {  // (np > 0 only in a version-3+ file)
     q += sizeof(int32_t) + sizeof(wk_prop) * np;
     HIPCHK(c, hipMemcpy(c->props, q, sizeof(float) * n * c->scene.pstride, hipMemcpyHostToDevice));
   }
@@ -1353,12 +1569,14 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
 static_assert(sizeof(wk_episode_rec) == sizeof(wk::EpisodeRecDev), "episode record layout");
 
 int wk_collect_data(wk_ctx* c, int on) {
+  DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   c->collect = on ? 1 : 0;
   return WK_OK;
 }
 
 int wk_episode_log_count(wk_ctx* c, int64_t* episodes, int64_t* updates) {
+  DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   uint64_t cnt = 0;
   HIPCHK(c, hipMemcpyAsync(&cnt, c->ep_count, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
@@ -1370,6 +1588,7 @@ int wk_episode_log_count(wk_ctx* c, int64_t* episodes, int64_t* updates) {
 
 int wk_episode_log_drain(wk_ctx* c, wk_episode_rec* out, int64_t cap, int64_t* n_out,
                          int64_t* dropped) {
+  DevGuard dg_(c);
   if (!c || cap < 0 || (cap > 0 && !out)) return WK_ERR_ARG;
   uint64_t cnt = 0;
   HIPCHK(c, hipMemcpyAsync(&cnt, c->ep_count, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
@@ -1389,6 +1608,7 @@ int wk_episode_log_drain(wk_ctx* c, wk_episode_rec* out, int64_t cap, int64_t* n
 
 int wk_loss_log_drain(wk_ctx* c, float* critic, float* actor, int64_t cap, int64_t* n_out,
                       int64_t* dropped) {
+  DevGuard dg_(c);
   if (!c || cap < 0 || (cap > 0 && (!critic || !actor))) return WK_ERR_ARG;
   const uint64_t kept = c->loss_count < c->loss_cap ? c->loss_count : c->loss_cap;
   if ((uint64_t)cap < kept) {

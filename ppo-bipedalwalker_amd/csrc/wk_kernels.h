@@ -23,6 +23,18 @@ struct PairTraceDev {
   float joint_impulse[4];
 };
 
+// physics event counters of the counting replay (wk_count_events; SURVEY 8(d) F_counted)
+enum : int {
+  EV_JOINT = 0,                            // Joint.Step past the 0.1 gap early-out
+  EV_AABB_LL, EV_AABB_LF, EV_AABB_BF,      // bounding boxes overlap -> SAT runs
+  EV_SAT_LL, EV_SAT_LF, EV_SAT_BF,         // SAT reports a collision -> contacts + MoveObjects
+  EV_IMP_LL, EV_IMP_LF, EV_IMP_BF,         // >= 1 contact point -> the impulse pair
+  EV_CONTACTS,                             // contact points found
+  EV_SUBSTEPS,                             // walker-substeps
+  EV_ENV_STEPS, EV_RESETS,                 // env-steps, auto-resets
+  NEV = 16                                 // (LL leg-leg, LF leg-floor, BF torso-floor)
+};
+
 struct StepArgs {
   float* st;                 // walker state records [n][NSTATE]
   const float* dxoff;        // [n] start offset (x = 125 + dx)
@@ -42,6 +54,7 @@ struct StepArgs {
   PairTraceDev* trace;       // [n][iterations] (TRACE)
   int k_steps;
   float* props;              // scene props [n][SceneDev::pstride] (k_env_scene) or null
+  unsigned long long* counts;  // [NEV] event totals (counting replay, mode 4) or null
 };
 
 // scene props (wk_scene.inc): Square / Triangle / Hexagon bodies after the floor, the same
@@ -99,6 +112,8 @@ hipError_t launch_policy(const EnvParams& P, const float* W, float lp_const, int
 hipError_t launch_returns(int n, int T, int use_gae, float gamma, float lambda, const float* r,
                           const float* v, const uint8_t* d, float* ret, float* adv, hipStream_t s);
 hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t s);
+hipError_t configure_device_kernels();  // dynamic-LDS attributes, current device (wk_create)
+hipError_t configure_mfma_kernels();
 hipError_t launch_ppo_grad_mfma(const GradArgs& g, int nblocks, hipStream_t s);
 hipError_t launch_swizzle(const float* W, float* Wz, hipStream_t s);
 int mfma_image_floats();

@@ -212,10 +212,12 @@ DEV Poly<N> perturbed(const Poly<N>& p) {
 // contact faces are evaluated in general, with Vector2.Normalize's NaN for a zero edge.
 template <int NA, int NB, bool BSTATIC, bool TRACE, int L, bool GENERIC = false>
 DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB,
-                      bool& colA, PairTraceDev* tr, int pi, int sub, RegionProf* rp = nullptr) {
+                      bool& colA, PairTraceDev* tr, int pi, int sub, RegionProf* rp = nullptr,
+                      uint32_t* ec = nullptr) {
   static_assert(!BSTATIC || NB == 4, "the static body is the floor");
   static_assert(!GENERIC || BSTATIC, "generic static floor polygon");
   constexpr bool FLAT = BSTATIC && !GENERIC;
+  constexpr int EVK = !BSTATIC ? 0 : (NA == 5 ? 2 : 1);  // leg-leg, leg-floor, torso-floor
   float mnx, mny, mxx, mxy;  // A's bounding box (the floor pass of sat_floor reuses it)
   aabb(A, mnx, mny, mxx, mxy);
   bool ov;
@@ -229,6 +231,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   rp_mark(rp, RP_AABB);
   DUP(1, { const auto Ap = perturbed(A); sink(aabb_overlap(Ap, B) ? 1.0f : 0.0f); });
   if (!ov) return;
+  if (ec) ec[EV_AABB_LL + EVK]++;
   if (TRACE && tr && pi >= 0) tr->aabb_hit[pi] = 1;
   if (BSTATIC) colA = true;  // body._isFloor -> Collided = true (:75)
   V2 n;
@@ -246,6 +249,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   DUP(2, { const auto Ap = perturbed(A); V2 n2; float d2;
            const bool h2 = sat(Ap, B, n2, d2); sink(n2.x); sink(n2.y); sink(d2); sink(h2 ? 1.0f : 0.0f); });
   if (!hit) return;
+  if (ec) ec[EV_SAT_LL + EVK]++;
   V2 c0, c1;
   int nc;
   if constexpr (KEEP && FLAT) nc = contact_points_ax(A, axa, B, floor_axes(), n, c0, c1);
@@ -271,7 +275,9 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
     move(B, vdiv(vmul(vneg(n), depth), 2.0f));
   }
   // Impulses.ResolveCollisions (Impulses.cs:12-28)
+  if (ec) ec[EV_CONTACTS] += (uint32_t)nc;
   if (nc == 0) return;
+  if (ec) ec[EV_IMP_LL + EVK]++;
   float e = net_maxf(mA.e, mB.e);
   float mu = net_minf(mA.mu, mB.mu);
   V2 contact = nc == 2 ? vdiv(vadd(c0, c1), 2.0f) : c0;
@@ -298,10 +304,11 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
 // Joint.Step (Objects/RigidBodies/Joint.cs:31-41); ResolveJoint swaps the bodies (:40)
 template <int NA, int NB, int IA, int IB, bool TRACE>
 DEV void joint_step(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB,
-                    PairTraceDev* tr, int ji) {
+                    PairTraceDev* tr, int ji, uint32_t* ec = nullptr) {
   V2 ab = vsub(mk(B.x[IB], B.y[IB]), mk(A.x[IA], A.y[IA]));
   float depth = vlen(ab);
   if (depth < 0.1f) return;
+  if (ec) ec[EV_JOINT]++;
   // ab.Normalize(): ab * (1 / sqrt(x^2 + y^2)), and that sqrt is depth (same correctly
   // rounded sqrt of the same sum); rcp_core is 1.0f / d bit for bit on [2^-48, 2^64]
   const float rinv = depth <= 0x1p63f ? rcp_core(depth) : 1.0f / depth;
@@ -346,7 +353,7 @@ DEV void rough_segment(Poly<4>& f, int k, float yprev, float y) {
 // heights in LDS, stride 64)
 template <int N, bool TRACE, int L, bool ROUGH>
 DEV void floor_pairs(Poly<N>& P, Dyn& D, const Mat& m, bool& col, PairTraceDev* tr, int pi,
-                     int sub, const float* ter) {
+                     int sub, const float* ter, uint32_t* ec = nullptr) {
   Dyn dfl;
   zero_dyn(dfl);
   const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};  // Metal, static: inverse mass/inertia 0
@@ -355,53 +362,54 @@ DEV void floor_pairs(Poly<N>& P, Dyn& D, const Mat& m, bool& col, PairTraceDev* 
     for (int k = 0; k < 10; k++) {
       Poly<4> seg;
       rough_segment(seg, k, ter[k * 64], ter[(k + 1) * 64]);
-      resolve_pair<N, 4, true, TRACE, L, true>(P, D, m, seg, dfl, mf, col, tr, -1, sub);
+      resolve_pair<N, 4, true, TRACE, L, true>(P, D, m, seg, dfl, mf, col, tr, -1, sub, nullptr, ec);
     }
   } else {
     Poly<4> fl;
     floor_poly(fl);
-    resolve_pair<N, 4, true, TRACE, L>(P, D, m, fl, dfl, mf, col, tr, pi, sub);
+    resolve_pair<N, 4, true, TRACE, L>(P, D, m, fl, dfl, mf, col, tr, pi, sub, nullptr, ec);
   }
 }
 
-// one substep of Environment.StepObjects (:130-142)
+// one substep of Environment.StepObjects (:130-142); ec: event counters (counting replay)
 template <bool TRACE, int L, bool ROUGH>
 DEV void substep(EnvState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
-                 PairTraceDev* tr, int sub, const float* ter) {
+                 PairTraceDev* tr, int sub, const float* ter, uint32_t* ec = nullptr) {
   // joints: [bodyJointLeft, bodyJointRight, leftJoint, rightJoint] (Walker.cs:182-187)
-  joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.llu, s.dllu, mp, tr, 0);
-  joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.rlu, s.drlu, mp, tr, 1);
-  joint_step<6, 6, 2, 3, TRACE>(s.llu, s.dllu, mp, s.lll, s.dlll, mp, tr, 2);
-  joint_step<6, 6, 2, 3, TRACE>(s.rlu, s.drlu, mp, s.rll, s.drll, mp, tr, 3);
+  joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.llu, s.dllu, mp, tr, 0, ec);
+  joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.rlu, s.drlu, mp, tr, 1, ec);
+  joint_step<6, 6, 2, 3, TRACE>(s.llu, s.dllu, mp, s.lll, s.dlll, mp, tr, 2, ec);
+  joint_step<6, 6, 2, 3, TRACE>(s.rlu, s.drlu, mp, s.rll, s.drll, mp, tr, 3, ec);
   // bodies in list order; the floor's own step is a no-op (static, zero velocity).
   // Episode 0 lists the floor last, every later episode first (Walker.cs:212-234):
   // that only changes the order of each leg segment's candidate pairs.
   integrate(s.lll, s.dlll, dt, adx, ady);
 #pragma unroll 1
   for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) floor_pairs<6, TRACE, L, ROUGH>(s.lll, s.dlll, mp, s.clll, tr, 1, sub, ter);
-    else resolve_pair<6, 6, false, TRACE, L>(s.lll, s.dlll, mp, s.llu, s.dllu, mp, s.clll, tr, 0, sub);
+    if ((q == 0) == s.post) floor_pairs<6, TRACE, L, ROUGH>(s.lll, s.dlll, mp, s.clll, tr, 1, sub, ter, ec);
+    else resolve_pair<6, 6, false, TRACE, L>(s.lll, s.dlll, mp, s.llu, s.dllu, mp, s.clll, tr, 0, sub, nullptr, ec);
   }
   integrate(s.llu, s.dllu, dt, adx, ady);
 #pragma unroll 1
   for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) floor_pairs<6, TRACE, L, ROUGH>(s.llu, s.dllu, mp, s.cllu, tr, 3, sub, ter);
-    else resolve_pair<6, 6, false, TRACE, L>(s.llu, s.dllu, mp, s.lll, s.dlll, mp, s.cllu, tr, 2, sub);
+    if ((q == 0) == s.post) floor_pairs<6, TRACE, L, ROUGH>(s.llu, s.dllu, mp, s.cllu, tr, 3, sub, ter, ec);
+    else resolve_pair<6, 6, false, TRACE, L>(s.llu, s.dllu, mp, s.lll, s.dlll, mp, s.cllu, tr, 2, sub, nullptr, ec);
   }
   integrate(s.body, s.dbody, dt, adx, ady);
-  floor_pairs<5, TRACE, L, ROUGH>(s.body, s.dbody, mb, s.cbody, tr, 4, sub, ter);
+  floor_pairs<5, TRACE, L, ROUGH>(s.body, s.dbody, mb, s.cbody, tr, 4, sub, ter, ec);
   integrate(s.rll, s.drll, dt, adx, ady);
 #pragma unroll 1
   for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) floor_pairs<6, TRACE, L, ROUGH>(s.rll, s.drll, mp, s.crll, tr, 6, sub, ter);
-    else resolve_pair<6, 6, false, TRACE, L>(s.rll, s.drll, mp, s.rlu, s.drlu, mp, s.crll, tr, 5, sub);
+    if ((q == 0) == s.post) floor_pairs<6, TRACE, L, ROUGH>(s.rll, s.drll, mp, s.crll, tr, 6, sub, ter, ec);
+    else resolve_pair<6, 6, false, TRACE, L>(s.rll, s.drll, mp, s.rlu, s.drlu, mp, s.crll, tr, 5, sub, nullptr, ec);
   }
   integrate(s.rlu, s.drlu, dt, adx, ady);
 #pragma unroll 1
   for (int q = 0; q < 2; q++) {
-    if ((q == 0) == s.post) floor_pairs<6, TRACE, L, ROUGH>(s.rlu, s.drlu, mp, s.crlu, tr, 8, sub, ter);
-    else resolve_pair<6, 6, false, TRACE, L>(s.rlu, s.drlu, mp, s.rll, s.drll, mp, s.crlu, tr, 7, sub);
+    if ((q == 0) == s.post) floor_pairs<6, TRACE, L, ROUGH>(s.rlu, s.drlu, mp, s.crlu, tr, 8, sub, ter, ec);
+    else resolve_pair<6, 6, false, TRACE, L>(s.rlu, s.drlu, mp, s.rll, s.drll, mp, s.crlu, tr, 7, sub, nullptr, ec);
   }
+  if (ec) ec[EV_SUBSTEPS]++;
 }
 
 // ---------------- policy (fused, weights read with wave-uniform scalar loads) ----------
@@ -554,8 +562,11 @@ DEV bool state_finite(const EnvState& s) {
 // L lanes per walker (a "row"): the Gauss-Seidel chain runs replicated in every lane of
 // the row (bit-identical state), SAT axes are split one per lane (sat_row); lane 0 of
 // the row owns all stores.  L = 1 is the plain one-walker-per-lane mapping.
-template <bool POLICY, bool RECORD, bool TRACE, int L, bool ROUGH>
+// COUNT (one lane per walker, flat floor, given actions): the counting replay -- the same
+// physics with per-lane event counters summed into A.counts (SURVEY 8(d) F_counted).
+template <bool POLICY, bool RECORD, bool TRACE, int L, bool ROUGH, bool COUNT = false>
 __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArgs A) {
+  static_assert(!COUNT || (L == 1 && !POLICY && !TRACE && !ROUGH), "counting replay");
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = tid / L, sub = tid % L;
   const int n = P.n_env;
@@ -582,6 +593,10 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArg
   const uint32_t gid = (uint32_t)(P.env_offset + e);
   uint32_t t = A.rng_t[e];
   uint32_t fault = 0;
+  uint32_t ecnt[NEV];
+#pragma unroll
+  for (int i = 0; i < NEV; i++) ecnt[i] = 0u;
+  uint32_t* const ec = COUNT ? ecnt : nullptr;
 
 #pragma unroll 1
   for (int k = 0; k < A.k_steps; k++) {
@@ -637,8 +652,9 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArg
         PairTraceDev z = {};
         *tr = z;
       }
-      substep<TRACE, L, ROUGH>(s, mp, mb, dt, adx, ady, tr, sub, ter);
+      substep<TRACE, L, ROUGH>(s, mp, mb, dt, adx, ady, tr, sub, ter, ec);
     }
+    if (COUNT) ecnt[EV_ENV_STEPS]++;
     // Walker.Update
     s.prevx = s.posx; s.prevy = s.posy;
     s.posx = s.body.cx; s.posy = s.body.cy;
@@ -664,6 +680,7 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArg
       make_template(s, dx);
       s.post = true;
       s.episodes = ep;
+      if (COUNT) ecnt[EV_RESETS]++;
     }
     if (leader) {
       if (A.obs_out) {
@@ -685,6 +702,15 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArg
     store_state(s, A.st, e, n);
     A.rng_t[e] = t;
     if (A.fault_out) A.fault_out[e] |= fault;
+  }
+  if constexpr (COUNT) {  // wave sums, one 64-bit atomic per counter and wave
+#pragma unroll
+    for (int i = 0; i < NEV; i++) {
+      uint32_t v = ecnt[i];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+      if ((threadIdx.x & 63) == 0 && v) atomicAdd(A.counts + i, (unsigned long long)v);
+    }
   }
 }
 
@@ -1231,6 +1257,12 @@ hipError_t launch_env_scene(int mode, const EnvParams& P, const StepArgs& A, con
   return hipGetLastError();
 }
 hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
+  if (mode == 4) {  // counting replay: one lane per walker, given actions, flat floor
+    if (P.rough || !A.counts || !A.actions) return hipErrorInvalidValue;
+    dim3 blk(64), grd((unsigned)((P.n_env + 63) / 64));
+    hipLaunchKernelGGL((k_env_step<false, false, false, 1, false, true>), grd, blk, 0, s, P, A);
+    return hipGetLastError();
+  }
   if (P.lanes == 2) launch_side(mode, P, A, s);
   else if (P.lanes == 16) launch_lanes<16>(mode, P, A, s);
   else launch_lanes<1>(mode, P, A, s);

@@ -416,14 +416,18 @@ __global__ void k_xavier(float* W, uint64_t seed) {
   W[p] = v;
 }
 
+// > 64 KiB of dynamic LDS (a gfx950 CU has 160 KiB) for every gradient kernel, on the
+// current device (called by wk_create after hipSetDevice)
+hipError_t configure_device_kernels() {
+  hipError_t e = hipFuncSetAttribute((const void*)k_ppo_grad<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_ppo_grad<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e == hipSuccess) e = configure_mfma_kernels();
+  return e;
+}
+
 hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t s) {
   const size_t lds = sizeof(float) * (L_WEND + SLAB + wpb * (64 * 4 + 24));
-  static bool attr_set = false;
-  if (!attr_set) {  // > 64 KiB of dynamic LDS (gfx950 CU has 160 KiB)
-    (void)hipFuncSetAttribute((const void*)k_ppo_grad<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_ppo_grad<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
   if (wpb == 1) {
     hipLaunchKernelGGL((k_ppo_grad<1>), dim3(nblocks), dim3(64), lds, s, g);
   } else {

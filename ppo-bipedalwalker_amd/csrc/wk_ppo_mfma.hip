@@ -455,6 +455,11 @@ hipError_t launch_swizzle(const float* W, float* Wz, hipStream_t s) {
   return hipGetLastError();
 }
 
+hipError_t configure_mfma_kernels() {
+  return hipFuncSetAttribute((const void*)k_ppo_grad_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)(sizeof(float) * mf::LDS_FLOATS));
+}
+
 int ppo_grad_mfma_blocks(int samples) {
   const int chunks = (samples + 15) / 16;
   int blocks = (chunks + mf::WAVES - 1) / mf::WAVES;
@@ -463,13 +468,6 @@ int ppo_grad_mfma_blocks(int samples) {
 
 hipError_t launch_ppo_grad_mfma(const GradArgs& g, int nblocks, hipStream_t s) {
   const size_t lds = sizeof(float) * mf::LDS_FLOATS;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_ppo_grad_mfma,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
   hipLaunchKernelGGL(k_ppo_grad_mfma, dim3(nblocks), dim3(64 * mf::WAVES), lds, s, g);
   return hipGetLastError();
 }

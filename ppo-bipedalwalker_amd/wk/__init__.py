@@ -17,6 +17,9 @@ STATE_FLOATS = 112
 NPARAM = 6149
 NPARAM_CRITIC = 897
 NPAIRS = 9
+NEV = 16  # WK_NEV event counters (wk_count_events)
+EVENTS = ["joint", "aabb_ll", "aabb_lf", "aabb_bf", "sat_ll", "sat_lf", "sat_bf", "imp_ll",
+          "imp_lf", "imp_bf", "contacts", "substeps", "env_steps", "resets", "r14", "r15"]
 ST_TORQUE, ST_POS, ST_PREV, ST_STEPS, ST_POSTRESET, ST_TERMINAL, ST_EPISODES = (
     100, 104, 106, 108, 109, 110, 111)
 MATERIALS = {"Carpet": 0, "Ice": 1, "Rubber": 2, "Metal": 3, "Wood": 4, "Paper": 5,
@@ -26,7 +29,7 @@ MATERIALS = {"Carpet": 0, "Ice": 1, "Rubber": 2, "Metal": 3, "Wood": 4, "Paper":
 EXPORTS = [
     "wk_config_defaults", "wk_version", "wk_create", "wk_destroy", "wk_last_error", "wk_sync",
     "wk_num_envs", "wk_reset", "wk_set_materials", "wk_set_offsets", "wk_step",
-    "wk_step_device", "wk_step_traced", "wk_get_obs", "wk_get_state", "wk_set_state",
+    "wk_step_device", "wk_step_sampled", "wk_step_traced", "wk_get_obs", "wk_get_state", "wk_set_state",
     "wk_get_body_view", "wk_set_scene", "wk_get_prop_view", "wk_get_weights", "wk_set_weights", "wk_get_adam", "wk_set_adam",
     "wk_policy_sample", "wk_value", "wk_rollout", "wk_rollout_stats_get", "wk_get_trajectory",
     "wk_set_trajectory", "wk_compute_returns", "wk_ppo_update", "wk_train_batch",
@@ -36,7 +39,7 @@ EXPORTS = [
     "wk_config_save_json", "wk_config_load_json", "wk_collect_data", "wk_episode_log_count",
     "wk_episode_log_drain", "wk_loss_log_drain", "wk_write_data_file",
     "wk_comm_unique_id", "wk_comm_init", "wk_allreduce_test", "wk_profile_enable",
-    "wk_profile_get", "wk_profile_reset",
+    "wk_profile_get", "wk_profile_reset", "wk_count_events", "wk_snapshot",
 ]
 
 
@@ -186,6 +189,7 @@ def load_library(path=None):
         "wk_step": (I, [P, P, I, P, P, P, P]),
         "wk_step_device": (I, [P, P, I, P, P, P, P]),
         "wk_step_traced": (I, [P, P, P]),
+        "wk_step_sampled": (I, [P, I, P, P, P, P, P, P, P, P]),
         "wk_get_obs": (I, [P, P]),
         "wk_get_state": (I, [P, P]),
         "wk_set_state": (I, [P, P]),
@@ -228,6 +232,8 @@ def load_library(path=None):
         "wk_profile_enable": (I, [P, I]),
         "wk_profile_get": (I, [P, C.POINTER(Profile)]),
         "wk_profile_reset": (I, [P]),
+        "wk_count_events": (I, [P, I, P]),
+        "wk_snapshot": (I, [P, I]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -401,6 +407,21 @@ class Engine:
         self._chk(self.lib.wk_step(self.h, _ptr(a), int(k), _ptr(obs), _ptr(rew), _ptr(done),
                                    _ptr(fault)), "wk_step")
         return obs, rew, done, fault
+
+    def step_sampled(self, k=1):
+        """Environment.Update with the agent's sampling (wk_step_sampled): the Trajectory
+        entries of Environment.cs:70-89 -- states before each step, unclipped actions,
+        per-dimension log-probabilities, values, rewards, dones -- and the next states."""
+        n = self.n
+        out = dict(states=np.empty((k, n, 12), np.float32), actions=np.empty((k, n, 4), np.float32),
+                   logp=np.empty((k, n, 4), np.float32), values=np.empty((k, n), np.float32),
+                   rewards=np.empty((k, n), np.float32), dones=np.empty((k, n), np.uint8),
+                   next_obs=np.empty((k, n, 12), np.float32), fault=np.empty(n, np.uint32))
+        self._chk(self.lib.wk_step_sampled(
+            self.h, int(k), _ptr(out["states"]), _ptr(out["actions"]), _ptr(out["logp"]),
+            _ptr(out["values"]), _ptr(out["rewards"]), _ptr(out["dones"]), _ptr(out["next_obs"]),
+            _ptr(out["fault"])), "wk_step_sampled")
+        return out
 
     def step_device(self, d_actions, k, d_obs, d_rew, d_done, d_fault):
         """Device-pointer variant (ints or None) on the context's stream; no sync."""
@@ -620,6 +641,20 @@ class Engine:
         x = _f32(x).copy()
         self._chk(self.lib.wk_allreduce_test(self.h, _ptr(x), x.size), "wk_allreduce_test")
         return x
+
+    # -- counting replay / snapshots --
+    def count_events(self, k):
+        """wk_count_events: replay the last rollout's first k action rows through the
+        counting kernel; returns the WK_NEV event totals (see include/wk_api.h)."""
+        c = np.zeros(NEV, np.uint64)
+        self._chk(self.lib.wk_count_events(self.h, int(k), _ptr(c)), "wk_count_events")
+        return c
+
+    def snapshot(self):
+        self._chk(self.lib.wk_snapshot(self.h, 0), "wk_snapshot")
+
+    def restore(self):
+        self._chk(self.lib.wk_snapshot(self.h, 1), "wk_snapshot")
 
     # -- profiling --
     def profile_enable(self, on=True):

@@ -112,23 +112,88 @@ def test_checkpoint_mismatch_rejected(wk, tmp_path):
     a.close()
 
 
-def test_checkpoint_version2_still_loads(wk, tmp_path):
-    """a version-2 file (no scene section: the layout before scene props) loads into a
-    context and clears its scene"""
+def _downgrade(raw, version):
+    """a version-4 file rewritten in an older layout: v3 drops the 16-byte CkptExt after the
+    48-byte header; v2 also drops the (empty) scene section's count"""
     import struct
+    assert struct.unpack_from("<I", raw, 4)[0] == 4 and raw[-4:] == b"\0\0\0\0"
+    out = bytearray(raw[:48] + raw[64:])
+    struct.pack_into("<I", out, 4, version)
+    return bytes(out if version == 3 else out[:-4])
+
+
+@pytest.mark.parametrize("version", [2, 3])
+def test_checkpoint_older_versions_still_load(wk, tmp_path, version):
+    """version-2 (no scene section: the layout before scene props) and version-3 files (no
+    RoughFloor record) load into a flat-floor context and clear its scene"""
     a = wk.Engine(64, seed=SEED, RandomizeStart=1)
     a.step(np.random.default_rng(1).uniform(-1, 1, (3, 64, 4)).astype(np.float32), k=3)
-    ck = tmp_path / "v3.ckpt"
+    ck = tmp_path / "v4.ckpt"
     a.checkpoint_save(ck)
-    raw = bytearray(ck.read_bytes())
-    assert struct.unpack_from("<I", raw, 4)[0] == 3 and raw[-4:] == b"\0\0\0\0"
-    struct.pack_into("<I", raw, 4, 2)
-    (tmp_path / "v2.ckpt").write_bytes(bytes(raw[:-4]))
+    old = tmp_path / f"v{version}.ckpt"
+    old.write_bytes(_downgrade(ck.read_bytes(), version))
     b = wk.Engine(64, seed=SEED)
     b.set_scene([wk.make_prop()])
-    b.checkpoint_load(tmp_path / "v2.ckpt")
+    b.checkpoint_load(old)
     np.testing.assert_array_equal(a.get_state(), b.get_state())
     with pytest.raises(wk.WkError):
         b.prop_view(0, 0)
     a.close()
     b.close()
+
+
+def test_rejected_checkpoint_leaves_context_unchanged(wk, tmp_path):
+    """every precondition is checked before the first device write: a file from
+    a different Iterations / MaxTimesteps / RoughFloor, or with scene props for a context that
+    cannot run them, is refused and the context's weights, Adam state, walkers and scene stay
+    as they were"""
+    rng = np.random.default_rng(3)
+    acts = rng.uniform(-1, 1, (2, 32, 4)).astype(np.float32)
+    cases = [(dict(Iterations=40), {}, "Iterations"),
+             (dict(MaxTimesteps=500), {}, "MaxTimesteps"),
+             (dict(RoughFloor=1), {}, "RoughFloor"),
+             ({}, dict(LanesPerWalker=2), "scene props")]
+    for i, (src_cfg, dst_cfg, what) in enumerate(cases):
+        src = wk.Engine(32, seed=SEED, **src_cfg)
+        if what == "scene props":
+            src.set_scene([wk.make_prop(cx=300.0, cy=700.0)])
+        src.step(acts, k=2)
+        ck = tmp_path / f"c{i}.ckpt"
+        src.checkpoint_save(ck)
+        dst = wk.Engine(32, seed=SEED + 0, RandomizeStart=1, **dst_cfg)
+        dst.step(acts[::-1].copy(), k=2)
+        dst.set_weights(dst.get_weights() * np.float32(0.5))
+        before = (dst.get_state(), dst.get_weights(), dst.get_adam())
+        with pytest.raises(wk.WkError, match=what):
+            dst.checkpoint_load(ck)
+        after = (dst.get_state(), dst.get_weights(), dst.get_adam())
+        np.testing.assert_array_equal(before[0], after[0])
+        np.testing.assert_array_equal(before[1], after[1])
+        for x, y in zip(before[2], after[2]):
+            np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
+        src.close()
+        dst.close()
+
+
+def test_contexts_on_two_devices(wk):
+    """every entry point binds the context's device, so two contexts on devices
+    0 and 1 used alternately from one thread keep their buffers and kernels apart, and the
+    caller's current device is left unchanged"""
+    torch = pytest.importorskip("torch")
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    rng = np.random.default_rng(5)
+    acts = rng.uniform(-1, 1, (4, 256, 4)).astype(np.float32)
+    torch.cuda.set_device(0)
+    a = wk.Engine(256, seed=SEED, device=0, RandomizeStart=1)
+    b = wk.Engine(256, seed=SEED, device=1, RandomizeStart=1)
+    ref = wk.Engine(256, seed=SEED, device=0, RandomizeStart=1)
+    for t in range(4):
+        a.step(acts[t:t + 1], k=1)
+        b.step(acts[t:t + 1], k=1)
+        ref.step(acts[t:t + 1], k=1)
+        assert torch.cuda.current_device() == 0
+    np.testing.assert_array_equal(a.get_state(), ref.get_state())
+    np.testing.assert_array_equal(b.get_state(), ref.get_state())
+    for e in (a, b, ref):
+        e.close()

@@ -372,8 +372,8 @@ def test_fast_sqrt_rcp_exhaustive():
 
 
 def test_baseline_config2_physics_4096(wk, orc):
-    """BASELINE config 2: 4,096 walkers, physics-step only (auto mapping = 16-lane rows
-    below 32,768 walkers), 10 env-steps with given actions, bit-exact vs the oracle."""
+    """BASELINE config 2: 4,096 walkers, physics-step only (auto mapping = the 2-lane leg
+    split at every size), 10 env-steps with given actions, bit-exact vs the oracle."""
     n, k = 4096, 10
     eng = wk.Engine(n, seed=SEED, RandomizeStart=1)
     assert eng.cfg.LanesPerWalker == 0
