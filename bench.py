@@ -5,12 +5,22 @@ One "step" = one PPO iteration over this rank's walkers: a device-resident rollo
 `--horizon` env-steps (policy sampling + 50 physics substeps + reward/terminal/auto-reset
 + value estimate, fused in one HIP kernel) followed by the returns scan and the PPO
 update (E epochs x pool/M minibatches: gradient kernel -> ordered reduction -> RCCL
-all-reduce -> Adam).  The metric's configuration (BASELINE.json: 65,536 walkers) fits one MI355X, so it is the
-N=1 workload; walkers are independent, so N GPUs run weakly scaled shards of --walkers
-each (65,536 per GPU) with only the policy-gradient all-reduce between them.
-value = env-steps of all ranks / max-over-ranks wall time.
+all-reduce -> Adam).
 
-  python bench.py [--gpus N --steps K --warmup W --walkers 8192 --horizon 64]
+Workload (BASELINE.json configs[3]): 65,536 walkers in total, sharded over the N GPUs
+(8,192 per GPU at N = 8), global minibatch 65,536 (M = 65,536 / N per GPU), T_h = 64, E = 5
+-- `scaling: strong`.  At N = 1 that is the metric's 65,536 walkers on one MI355X.
+`--walkers W` instead fixes W walkers per GPU (`scaling: weak`).
+
+Regime: throughput depends on where training is (episode lengths change the reset / contact
+mix), so the bench runs a fixed `--regime-iters` iterations from the seeded initial state,
+snapshots the whole training state on the device (wk_snapshot), and every warm-up and timed
+iteration restores it first (a ~30 MB device copy, inside the timed region): each timed
+step is the same iteration, whatever --steps / --warmup the driver passes.
+
+value = env-steps of all ranks / max-over-ranks wall time of the K timed steps.
+
+  python bench.py [--gpus N --steps K --warmup W --walkers-global 65536 --horizon 64]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 """
 import argparse
@@ -23,12 +33,27 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ppo-bipedalwalker_amd"))
 
 METRIC = "env-steps/sec (whole node) + PPO-update ms, 65k walkers at 1/2/4/8 MI355X"
-# algorithmic fp32 flops per env-step (50 substeps x 5,775 + actor
-# forward 10,504 + sampling/log-prob/obs/reward ~130) and bytes per env-step.
-FLOP_PER_ENV_STEP = 3.0e5
-BYTES_PER_ENV_STEP = 950.0
-PEAK_FP32_TFLOPS = 157.3   # MI355X fp32 vector (= fp32 matrix) peak, MI355X_MICROARCH.md
+# MI355X_MICROARCH.md: fp32 vector peak 157.3 TF counts an FMA as 2 flops at the packed
+# (v_pk_fma_f32) rate.  The physics is restated op for op with no FMA contraction (parity),
+# so its honest ceilings are the packed mul/add rate (78.6 T flop/s) and, for the scalar
+# ops that dominate the dependent chains, the non-packed issue rate (39.3 T op/s:
+# 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz).
+PEAK_FP32_TFLOPS = 157.3
+PEAK_NOFMA_PACKED = 78.6
+PEAK_NOFMA_SCALAR = 39.3
 PEAK_HBM_GBS = 8000.0
+# SURVEY.md 8(d) flop model, priced per counted physics event (wk_count_events):
+FLOP_INTEGRATE = 477          # per walker-substep: 4 poles x 95 + hull 81 + floor 16
+FLOP_JOINT = 107              # per Joint.Step past the 0.1 early-out ((2x106 + 2x108) / 4)
+FLOP_SAT = {"ll": 571, "lf": 417, "bf": 349}       # (VA+VB)(11+3(VA+VB))+7, per AABB hit
+FLOP_CONTACT = {"ll": 190, "lf": 166, "bf": 161}   # contact clipping + MoveObjects, per SAT hit
+FLOP_IMPULSE = 110            # normal + friction impulse pair, per resolution with contacts
+FLOP_POLICY = 10504 + 1793 + 130  # actor + critic forward, sampling / log-prob, obs / reward
+FLOP_UPPER = 3.0e5            # SURVEY's all-pairs-colliding upper bound per env-step
+# algorithmic HBM bytes per env-step of the rollout: trajectory row 89 B +
+# the 448-B walker record read and written once per T_h = 64 env-steps
+def alg_bytes_per_env_step(horizon):
+    return 89.0 + 2 * 448.0 / horizon
 
 
 def parse():
@@ -36,23 +61,72 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--walkers", type=int, default=65536, help="walkers per GPU")
+    p.add_argument("--walkers-global", type=int, default=65536,
+                   help="walkers over all GPUs (strong scaling, BASELINE config 4)")
+    p.add_argument("--walkers", type=int, default=0,
+                   help="walkers per GPU instead (weak scaling)")
     p.add_argument("--horizon", type=int, default=64)
     p.add_argument("--epochs", type=int, default=5)
-    p.add_argument("--minibatch", type=int, default=0, help="per-GPU minibatch (0 = walkers)")
+    p.add_argument("--minibatch-global", type=int, default=0,
+                   help="global minibatch (0 = all walkers: 65,536)")
     p.add_argument("--materials", action="store_true", help="config 5: random Ice/Rubber/Carpet")
     p.add_argument("--seed", type=int, default=20250905)
     p.add_argument("--lanes", type=int, default=0,
                    help="lanes per walker in the physics kernel (0 auto, 1, 2 or 16)")
+    p.add_argument("--regime-iters", type=int, default=8,
+                   help="PPO iterations from the seeded start before the snapshot")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the configs 2 / 3 / 4-shard / 5-shard lines (N = 1 only)")
     p.add_argument("--cpu-baseline-steps", type=int, default=150000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_physics.json"))
     return p.parse_args()
 
 
+# ---------------------------------------------------------------- CPU baseline ----------
+_CPU_WORKER = """
+import sys, time
+sys.path.insert(0, sys.argv[1])
+import orc
+n, env, seed, t_start = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), float(sys.argv[5])
+orc.physics_loop(200, seed=seed, env=env)  # load + warm
+while time.time() < t_start:
+    time.sleep(0.001)
+t0 = time.perf_counter()
+orc.reference_loop(n, seed=seed, env=env)
+print(time.perf_counter() - t0)
+"""
+
+
+def _all_cores(threads, n_each, seed):
+    """one walker per process (the reference loop), all processes started together; child
+    processes with no GPU (subprocess: fork + exec before anything touches a device)"""
+    import subprocess
+    t_start = time.time() + 2.0
+    procs = [subprocess.Popen([sys.executable, "-c", _CPU_WORKER, os.path.join(ROOT, "oracle"),
+                               str(n_each), str(i), str(seed), repr(t_start)],
+                              stdout=subprocess.PIPE, text=True) for i in range(threads)]
+    secs = [float(p.communicate()[0].strip().splitlines()[-1]) for p in procs]
+    if any(p.returncode for p in procs):
+        raise RuntimeError("a CPU baseline worker failed")
+    return threads * n_each / max(secs)
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args):
-    """The oracle's single-walker reference loop (Game1.Update -> Environment.Update with
-    Train at every terminal step, 5 epochs x floor(T/64) x 64), on one host core."""
+    """the oracle (C restatement of the reference's single-threaded C#
+    loop) on the host cores: (i) 1 walker on 1 core -- the full loop (policy + physics +
+    Train at every episode end), physics only, and Train ms per 1001-step episode; (ii) one
+    walker per process on the box's CPU share."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc
     orc.build()
@@ -60,28 +134,135 @@ def cpu_baseline(args):
     t0 = time.perf_counter()
     eps, train_s = orc.reference_loop(n, seed=args.seed)
     dt = time.perf_counter() - t0
+    n_phys = max(1000, n // 2)
+    t0 = time.perf_counter()
+    orc.physics_loop(n_phys, seed=args.seed)
+    dt_phys = time.perf_counter() - t0
+    train_ms = min(orc.train_episode_seconds(1001, seed=args.seed) for _ in range(3)) * 1e3
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    threads = max(1, min(16, avail))  # the box's CPU share for one GPU is 16
+    n_each = max(1000, n // 4)
+    all_rate = _all_cores(threads, n_each, args.seed)
     return {"value": n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} env-steps of the single-walker reference loop (policy + physics, "
-                      f"PPO Train at each of {eps} episode ends: {train_s:.2f} s of {dt:.2f} s)"}
+            "sample": (f"{n} env-steps of the single-walker reference loop (policy + physics, "
+                       f"PPO Train at each of {eps} episode ends: {train_s:.2f} s of {dt:.2f} s)"),
+            "physics_only_env_steps_per_s": n_phys / dt_phys,
+            "physics_only_sample": f"{n_phys} env-steps, one walker, uniform synthetic actions",
+            "train_ms_per_1001_step_episode": train_ms,
+            "all_cores": {"threads": threads, "env_steps_per_s": all_rate,
+                          "sample": f"{threads} processes x {n_each} env-steps of the reference loop",
+                          "nproc": os.cpu_count(), "affinity_cpus": avail,
+                          "cpu_model": _cpu_model()}}
+
+
+# ---------------------------------------------------------------- GPU -------------------
+def flops_per_env_step(ev):
+    """SURVEY 8(d)'s per-primitive constants priced on the counted events"""
+    f = FLOP_INTEGRATE * ev["substeps"] + FLOP_JOINT * ev["joint"] + FLOP_IMPULSE * (
+        ev["imp_ll"] + ev["imp_lf"] + ev["imp_bf"])
+    for c in ("ll", "lf", "bf"):
+        f += FLOP_SAT[c] * ev["aabb_" + c] + FLOP_CONTACT[c] * ev["sat_" + c]
+    return f / ev["env_steps"] + FLOP_POLICY
+
+
+def time_iterations(eng, args, k, horizon, update_index, barrier=None, physics_only=None):
+    """k iterations, each restoring the snapshot; returns wall seconds"""
+    if barrier:
+        barrier()
+    else:
+        eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        eng.restore()
+        if physics_only is not None:
+            physics_only()
+        else:
+            eng.rollout(horizon)
+            eng.ppo_update(update_index=update_index, sync=False)
+    if barrier:
+        eng.sync()
+        barrier()
+    else:
+        eng.sync()
+    return time.perf_counter() - t0
+
+
+def extra_config(wk, torch, args, n, M, M_global, horizon, physics_only=False, materials=False,
+                 k=5):
+    """one of BASELINE's other shapes on this GPU (same regime protocol as the main line)"""
+    eng = wk.Engine(n, seed=args.seed, Horizon=horizon, Minibatch=M, MinibatchGlobal=M_global,
+                    Epochs=args.epochs, RandomizeStart=1, RandomizeMaterial=int(materials),
+                    LanesPerWalker=args.lanes)
+    try:
+        if physics_only:
+            g = torch.Generator(device="cuda").manual_seed(args.seed)
+            acts = torch.rand((horizon, n, 4), device="cuda", generator=g) * 2 - 1
+            rew = torch.empty((horizon, n), device="cuda")
+            done = torch.empty((horizon, n), device="cuda", dtype=torch.uint8)
+            torch.cuda.synchronize()
+            step = lambda: eng.step_device(acts.data_ptr(), horizon, None, rew.data_ptr(),
+                                           done.data_ptr(), None)
+            eng.snapshot()
+            time_iterations(eng, args, 2, horizon, 0, physics_only=step)  # warm-up
+            dt = time_iterations(eng, args, 16, horizon, 0, physics_only=step)
+            return {"walkers": n, "env_steps_timed": 16 * n * horizon,
+                    "env_steps_per_s": 16 * n * horizon / dt}
+        for it in range(args.regime_iters):
+            eng.rollout(horizon)
+            eng.ppo_update(update_index=it, sync=False)
+        eng.snapshot()
+        time_iterations(eng, args, 1, horizon, args.regime_iters)
+        eng.profile_reset()
+        eng.profile_enable(1)
+        dt = time_iterations(eng, args, k, horizon, args.regime_iters)
+        prof = eng.profile()
+        eng.profile_enable(0)
+        return {"walkers": n, "minibatch": M, "minibatch_global": M_global,
+                "env_steps_per_s": k * n * horizon / dt,
+                "rollout_ms": prof["physics_ms"] / max(1, prof["physics_launches"]),
+                "rollout_env_steps_per_s": n * horizon * prof["physics_launches"]
+                / max(1e-9, prof["physics_ms"] * 1e-3),
+                "ppo_update_ms": prof["update_ms"] / max(1, prof["update_calls"]),
+                "minibatches_per_update": args.epochs * (n * horizon // M)}
+    finally:
+        eng.close()
 
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
     import wk
     from wk.dist import broadcast_unique_id, env_from_launcher, make_shard
 
     rank, world, local = env_from_launcher()
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    # the CPU leg first, before this process touches the GPU (its workers are spawned)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    import torch
+    import torch.distributed as dist
     if world > 1:
         dist.init_process_group("gloo")  # control plane only; gradients go over RCCL
     torch.cuda.set_device(local)
-    shard = make_shard(rank, world, local, args.walkers, args.minibatch or args.walkers)
-    eng = wk.Engine(shard.n_local, seed=args.seed, device=local, Horizon=args.horizon,
+    weak = args.walkers > 0
+    if weak:
+        n_local = args.walkers
+        m_global = args.minibatch_global or n_local * world
+    else:
+        if args.walkers_global % world:
+            raise SystemExit("--walkers-global must divide by the number of GPUs")
+        n_local = args.walkers_global // world
+        m_global = args.minibatch_global or args.walkers_global
+    if m_global % world:
+        raise SystemExit("the global minibatch must divide by the number of GPUs")
+    shard = make_shard(rank, world, local, n_local, m_global // world)
+    T = args.horizon
+    eng = wk.Engine(shard.n_local, seed=args.seed, device=local, Horizon=T,
                     Minibatch=shard.minibatch_local, MinibatchGlobal=shard.minibatch_global,
                     Epochs=args.epochs, EnvOffset=shard.env_offset, RandomizeStart=1,
                     RandomizeMaterial=1 if args.materials else 0, LanesPerWalker=args.lanes)
@@ -96,57 +277,54 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    it = 0
-    for _ in range(args.warmup):
-        eng.rollout(args.horizon)
+    # fixed regime: R iterations from the seeded start, then the device snapshot
+    for it in range(args.regime_iters):
+        eng.rollout(T)
         eng.ppo_update(update_index=it, sync=False)
-        it += 1
-    barrier()
+    eng.snapshot()
+    upd = args.regime_iters
+    time_iterations(eng, args, args.warmup, T, upd, barrier)
     eng.profile_reset()
     eng.profile_enable(1)  # one HIP event pair per rollout launch and per whole update
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.rollout(args.horizon)
-        eng.ppo_update(update_index=it, sync=False)
-        it += 1
-    eng.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed = time_iterations(eng, args, args.steps, T, upd, barrier)
     prof = eng.profile()
-    stats = eng.rollout_stats()
-    # one more (untimed) iteration with an event pair around every kernel launch
+    eng.profile_enable(0)
+    # untimed: one iteration with an event pair around every kernel launch
     eng.profile_reset()
     eng.profile_enable(2)
-    eng.rollout(args.horizon)
-    eng.ppo_update(update_index=it, sync=False)
-    eng.sync()
+    time_iterations(eng, args, 1, T, upd)
     eng.profile_enable(0)
     prof_k = eng.profile()
+    # untimed: the same rollout's physics events (counting replay of its actions)
+    eng.restore()
+    eng.rollout(T)
+    stats = eng.rollout_stats()
+    eng.restore()
+    ev = dict(zip(wk.EVENTS, eng.count_events(T).tolist()))
 
-    t = torch.tensor([elapsed, prof["physics_ms"], prof["update_ms"] + prof["returns_ms"]],
-                     dtype=torch.float64)
+    t = torch.tensor([elapsed, prof["physics_ms"], prof["update_ms"]], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, phys_ms_max, upd_ms_max = t.tolist()
 
-    env_steps = world * shard.n_local * args.horizon * args.steps
+    env_steps = world * shard.n_local * T * args.steps
     value = env_steps / elapsed
-    phys_launch_ms = prof["physics_ms"] / max(1, prof["physics_launches"])
-    units_per_launch = prof["physics_env_steps"] / max(1, prof["physics_launches"])
-    achieved_tflops = FLOP_PER_ENV_STEP * units_per_launch / (phys_launch_ms * 1e-3) / 1e12
+    launch_ms = prof["physics_ms"] / max(1, prof["physics_launches"])
+    units = prof["physics_env_steps"] / max(1, prof["physics_launches"])
+    f_counted = flops_per_env_step(ev)
+    achieved = f_counted * units / (launch_ms * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_file):
         try:
             tj = json.load(open(args.traffic_file))
-            if tj.get("walkers") == shard.n_local and tj.get("horizon") == args.horizon:
+            if tj.get("walkers") == shard.n_local and tj.get("horizon") == T:
                 traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
+        except (OSError, ValueError):
             traffic = None
-    ppo_update_ms = upd_ms_max / args.steps
+    lanes = args.lanes or 2
+    kernel = {2: "k_env_side<true,true,false>", 16: "k_env_step<true,true,false,16,false>",
+              1: "k_env_step<true,true,false,1,false>"}[lanes]
+    alg_bytes = alg_bytes_per_env_step(T) * units
     out = {
         "metric": METRIC,
         "value": value,
@@ -156,45 +334,65 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (Philox-randomised start offsets; random-init Xavier policy)",
         "config": {
-            "workload": ("BASELINE config 4 walker count (65,536) per GPU, config 3 step: "
-                         f"{shard.n_local} walkers/GPU, rollout T_h={args.horizon} with policy "
-                         f"sampling + PPO update E={args.epochs}, M={shard.minibatch_local}/GPU"
+            "workload": (f"BASELINE config 4: {shard.n_local * world} walkers over {world} GPU(s) "
+                         f"({shard.n_local}/GPU), config 3 step: rollout T_h={T} with policy "
+                         f"sampling + PPO update E={args.epochs}, global minibatch "
+                         f"{shard.minibatch_global} ({shard.minibatch_local}/GPU)"
                          + (", per-env Ice/Rubber/Carpet (config 5)" if args.materials else "")),
             "walkers_per_gpu": shard.n_local,
             "global_walkers": shard.n_local * world,
-            "horizon": args.horizon,
+            "horizon": T,
             "epochs": args.epochs,
             "minibatch_global": shard.minibatch_global,
             "parallelism": f"dp{world}",
         },
-        "ppo_update_ms": ppo_update_ms,
-        "rollout_env_steps_per_s": world * shard.n_local * args.horizon * args.steps / (phys_ms_max * 1e-3),
+        "ppo_update_ms": upd_ms_max / args.steps,
+        "rollout_env_steps_per_s": world * shard.n_local * T * args.steps / (phys_ms_max * 1e-3),
+        "regime": {"iterations_before_snapshot": args.regime_iters,
+                   "episodes_per_rollout": int(stats.episodes)},
         "roofline": {
-            "bound": "mfma",
-            "kernel": {2: "k_env_side<true,true,false>", 16: "k_env_step<true,true,false,16>",
-                       1: "k_env_step<true,true,false,1>"}[args.lanes or (2 if shard.n_local >= 32768 else 16)]
-                      + " (fused rollout: physics + policy)",
-            "achieved": achieved_tflops,
+            "bound": "valu",
+            "kernel": kernel + " (fused rollout: physics + matrix-core policy)",
+            "achieved": achieved,
             "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s",
-            "frac": achieved_tflops / PEAK_FP32_TFLOPS,
+            "frac": achieved / PEAK_FP32_TFLOPS,
             "traffic": traffic,
-            "note": ("fp32 compute-bound (VALU; the MI355X fp32 vector peak equals the fp32 "
-                     "MFMA peak, 157.3 TF); algorithmic flops = 3.0e5 per env-step (SURVEY 8(d)) "
-                     f"x {units_per_launch:.0f} env-steps per launch / {phys_launch_ms:.3f} ms "
-                     "mean launch (HIP events on the engine stream)"),
-            "hbm_frac": BYTES_PER_ENV_STEP * units_per_launch / (phys_launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+            "peak_no_fma_packed": PEAK_NOFMA_PACKED,
+            "frac_no_fma_packed": achieved / PEAK_NOFMA_PACKED,
+            "peak_no_fma_scalar_issue": PEAK_NOFMA_SCALAR,
+            "frac_no_fma_scalar_issue": achieved / PEAK_NOFMA_SCALAR,
+            "flop_per_env_step_counted": f_counted,
+            "flop_per_env_step_upper_bound": FLOP_UPPER,
+            "events_per_env_step": {k: v / ev["env_steps"] for k, v in ev.items()
+                                    if not k.startswith("r1") and k != "env_steps"},
+            "hbm_GBs": (traffic / (launch_ms * 1e-3) / 1e9) if traffic else None,
+            "hbm_frac": (traffic / (launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBS) if traffic else None,
+            "alg_bytes_per_launch": alg_bytes,
+            "note": ("VALU-issue bound (op-for-op fp32 restatement, no FMA contraction); achieved = "
+                     f"F_counted {f_counted:.0f} flop/env-step (SURVEY 8(d) constants priced on "
+                     f"this rollout's counted AABB/SAT/contact/impulse/joint events) x "
+                     f"{units:.0f} env-steps per launch / {launch_ms:.3f} ms mean launch (HIP "
+                     "events on the engine stream)"),
         },
         "kernel_ms_one_step": {k: v for k, v in prof_k.items() if k.endswith("_ms")},
-        "episodes_last_rollout": stats.episodes,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0 and world == 1 and not args.no_extras:
+        ex = {}
+        ex["config2_physics_4096"] = extra_config(wk, torch, args, 4096, 4096, 4096, T,
+                                                  physics_only=True)
+        ex["config3_full_4096"] = extra_config(wk, torch, args, 4096, 4096, 4096, T)
+        ex["config4_shard_8192"] = extra_config(wk, torch, args, 8192, 8192, 65536, T)
+        ex["config5_shard_8192"] = extra_config(wk, torch, args, 8192, 8192, 65536, T,
+                                                materials=True)
+        out["configs"] = ex
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

@@ -115,6 +115,9 @@ def lib():
             "orc_returns_gae": (None, [I, P, P, P, F, F, P, P]),
             "orc_normalize": (None, [I, P, F]),
             "orc_reference_loop": (I, [C.POINTER(Hyper), U64, I, C.POINTER(C.c_double)]),
+            "orc_reference_loop_env": (I, [C.POINTER(Hyper), U64, I, I, C.POINTER(C.c_double)]),
+            "orc_physics_loop": (I, [C.POINTER(Hyper), U64, I, I]),
+            "orc_train_episode_seconds": (C.c_double, [C.POINTER(Hyper), U64, I]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -364,8 +367,22 @@ def contacts(va, vb, normal):
     return out[:2 * k].reshape(k, 2)
 
 
-def reference_loop(n_steps, seed=20250905, **hkw):
+def reference_loop(n_steps, seed=20250905, env=0, **hkw):
+    """the reference's single-walker Game1.Update loop (policy + physics, Train at every
+    episode end); returns (episodes, seconds spent in Train)"""
     h = hyper(**hkw)
     tt = C.c_double()
-    eps = lib().orc_reference_loop(C.byref(h), int(seed), int(n_steps), C.byref(tt))
+    eps = lib().orc_reference_loop_env(C.byref(h), int(seed), int(env), int(n_steps), C.byref(tt))
     return eps, tt.value
+
+
+def physics_loop(n_steps, seed=20250905, env=0, **hkw):
+    """one walker, physics only, uniform synthetic actions; returns episodes"""
+    h = hyper(**hkw)
+    return lib().orc_physics_loop(C.byref(h), int(seed), int(env), int(n_steps))
+
+
+def train_episode_seconds(T=1001, seed=20250905, **hkw):
+    """wall seconds of one PPOAgent.Train(Trajectory) on a T-step episode"""
+    h = hyper(**hkw)
+    return lib().orc_train_episode_seconds(C.byref(h), int(seed), int(T))

@@ -391,9 +391,56 @@ void orc_normalize(int n, float* x, float eps_clip) {
   }
 }
 
+/* PPOAgent.Train(Trajectory) (PPOAgent.cs:147-172) on one episode of T steps: value
+ * estimates (:447-456), returns / advantages (:175-189), then Epochs x floor(T / BatchSize)
+ * minibatches drawn without replacement (CreateBatches :501-540, keyed permutation for the
+ * unseeded Random), each Train(Batch) + Adam (:218-346). */
+void orc_train_trajectory(orc_agent* ag, const orc_hyper* h, uint64_t seed, uint32_t update, int T,
+                          const float* S, const float* Ac, const float* Lp, const float* R) {
+  float* Vv = (float*)malloc(sizeof(float) * (T + 1));
+  float* G = (float*)malloc(sizeof(float) * (T + 1));
+  float* Ad = (float*)malloc(sizeof(float) * (T + 1));
+  float* bS = (float*)malloc(sizeof(float) * 12 * h->BatchSize);
+  float* bA = (float*)malloc(sizeof(float) * 4 * h->BatchSize);
+  float* bL = (float*)malloc(sizeof(float) * 4 * h->BatchSize);
+  float* bG = (float*)malloc(sizeof(float) * h->BatchSize);
+  float* bAd = (float*)malloc(sizeof(float) * h->BatchSize);
+  for (int i = 0; i < T; i++) Vv[i] = orc_critic_value(ag, S + 12 * i);
+  if (h->UseGAE) orc_returns_gae(T, R, Vv, NULL, h->Gamma, h->Lambda, G, Ad);
+  else orc_returns_mc(T, R, Vv, NULL, h->Gamma, G, Ad);
+  if (h->NormalizeAdvantages) orc_normalize(T, Ad, h->Epsilon);
+  int nb = T / h->BatchSize;
+  for (int ep = 0; ep < h->Epochs; ep++) {
+    uint32_t key[4];
+    orc_perm_key(seed, update, (uint32_t)ep, key);
+    for (int b = 0; b < nb; b++) {
+      for (int k = 0; k < h->BatchSize; k++) {
+        uint32_t idx = orc_perm((uint32_t)(b * h->BatchSize + k), (uint32_t)T, key);
+        memcpy(bS + 12 * k, S + 12 * idx, sizeof(float) * 12);
+        memcpy(bA + 4 * k, Ac + 4 * idx, sizeof(float) * 4);
+        memcpy(bL + 4 * k, Lp + 4 * idx, sizeof(float) * 4);
+        bG[k] = G[idx];
+        bAd[k] = Ad[idx];
+      }
+      orc_train_batch(ag, h->BatchSize, (float)h->BatchSize, bS, bA, bL, bG, bAd, NULL, NULL,
+                      NULL, 1);
+    }
+  }
+  free(Vv); free(G); free(Ad);
+  free(bS); free(bA); free(bL); free(bG); free(bAd);
+}
+
+static double now_s(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
 /* Game1.Update x n_steps on one walker with Train at every terminal step: the
- * reference's own single-threaded loop (CPU baseline workload). */
-int orc_reference_loop(const orc_hyper* h, uint64_t seed, int n_steps, double* train_seconds) {
+ * reference's own single-threaded loop (CPU baseline workload).  env selects the walker's
+ * Philox streams (one walker per thread in the all-cores baseline). */
+int orc_reference_loop_env(const orc_hyper* h, uint64_t seed, int env_id, int n_steps,
+                           double* train_seconds) {
   orc_env* env = orc_env_create(h, 0.0f, ORC_MAT_CARPET);
   orc_agent* ag = orc_agent_create(h, seed);
   int cap = h->MaxTimesteps + 2;
@@ -401,14 +448,6 @@ int orc_reference_loop(const orc_hyper* h, uint64_t seed, int n_steps, double* t
   float* Ac = (float*)malloc(sizeof(float) * 4 * cap);
   float* Lp = (float*)malloc(sizeof(float) * 4 * cap);
   float* R = (float*)malloc(sizeof(float) * cap);
-  float* Vv = (float*)malloc(sizeof(float) * cap);
-  float* G = (float*)malloc(sizeof(float) * cap);
-  float* Ad = (float*)malloc(sizeof(float) * cap);
-  float* bS = (float*)malloc(sizeof(float) * 12 * h->BatchSize);
-  float* bA = (float*)malloc(sizeof(float) * 4 * h->BatchSize);
-  float* bL = (float*)malloc(sizeof(float) * 4 * h->BatchSize);
-  float* bG = (float*)malloc(sizeof(float) * h->BatchSize);
-  float* bAd = (float*)malloc(sizeof(float) * h->BatchSize);
   float state[12];
   orc_env_get_obs(env, state);
   int T = 0, episodes = 0;
@@ -416,47 +455,71 @@ int orc_reference_loop(const orc_hyper* h, uint64_t seed, int n_steps, double* t
   double tt = 0.0;
   for (int it = 0; it < n_steps; it++) {
     memcpy(S + 12 * T, state, sizeof(state));
-    orc_sample_actions(ag, state, seed, 0, gstep++, Ac + 4 * T, Lp + 4 * T);
+    orc_sample_actions(ag, state, seed, env_id, gstep++, Ac + 4 * T, Lp + 4 * T);
     float rew;
     int done;
     orc_env_step(env, Ac + 4 * T, state, &rew, &done, NULL);
     R[T] = rew;
     T++;
     if (done) {
-      struct timespec t0, t1;
-      clock_gettime(CLOCK_MONOTONIC, &t0);
-      for (int i = 0; i < T; i++) Vv[i] = orc_critic_value(ag, S + 12 * i);
-      if (h->UseGAE) orc_returns_gae(T, R, Vv, NULL, h->Gamma, h->Lambda, G, Ad);
-      else orc_returns_mc(T, R, Vv, NULL, h->Gamma, G, Ad);
-      if (h->NormalizeAdvantages) orc_normalize(T, Ad, h->Epsilon);
-      int nb = T / h->BatchSize;
-      for (int ep = 0; ep < h->Epochs; ep++) {
-        uint32_t key[4];
-        orc_perm_key(seed, update, (uint32_t)ep, key);
-        for (int b = 0; b < nb; b++) {
-          for (int k = 0; k < h->BatchSize; k++) {
-            uint32_t idx = orc_perm((uint32_t)(b * h->BatchSize + k), (uint32_t)T, key);
-            memcpy(bS + 12 * k, S + 12 * idx, sizeof(float) * 12);
-            memcpy(bA + 4 * k, Ac + 4 * idx, sizeof(float) * 4);
-            memcpy(bL + 4 * k, Lp + 4 * idx, sizeof(float) * 4);
-            bG[k] = G[idx];
-            bAd[k] = Ad[idx];
-          }
-          orc_train_batch(ag, h->BatchSize, (float)h->BatchSize, bS, bA, bL, bG, bAd, NULL, NULL,
-                          NULL, 1);
-        }
-      }
+      const double t0 = now_s();
+      orc_train_trajectory(ag, h, seed, update, T, S, Ac, Lp, R);
+      tt += now_s() - t0;
       update++;
-      clock_gettime(CLOCK_MONOTONIC, &t1);
-      tt += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
       episodes++;
       T = 0;
     }
   }
   if (train_seconds) *train_seconds = tt;
-  free(S); free(Ac); free(Lp); free(R); free(Vv); free(G); free(Ad);
-  free(bS); free(bA); free(bL); free(bG); free(bAd);
+  free(S); free(Ac); free(Lp); free(R);
   orc_agent_destroy(ag);
   orc_env_destroy(env);
   return episodes;
+}
+
+int orc_reference_loop(const orc_hyper* h, uint64_t seed, int n_steps, double* train_seconds) {
+  return orc_reference_loop_env(h, seed, 0, n_steps, train_seconds);
+}
+
+/* Environment.Update without the agent (physics only, Environment.cs:126-143 + reward /
+ * terminal / reset): one walker, uniform actions in [-1, 1] from Philox (BASELINE config 2's
+ * synthetic actions); returns the number of episodes. */
+int orc_physics_loop(const orc_hyper* h, uint64_t seed, int env_id, int n_steps) {
+  orc_env* env = orc_env_create(h, orc_env_offset(seed, env_id), ORC_MAT_CARPET);
+  float a[4], obs[12], rew;
+  int done, episodes = 0;
+  for (int t = 0; t < n_steps; t++) {
+    orc_synth_action(seed, env_id, (uint32_t)t, a);
+    orc_env_step(env, a, obs, &rew, &done, NULL);
+    episodes += done;
+  }
+  orc_env_destroy(env);
+  return episodes;
+}
+
+/* seconds for one Train(Trajectory) on a T-step episode (the reference trains once per
+ * episode; T = 1001 is a full-length one): the trajectory is sampled by the agent on the
+ * walker, continuing through resets so any T is available. */
+double orc_train_episode_seconds(const orc_hyper* h, uint64_t seed, int T) {
+  orc_env* env = orc_env_create(h, 0.0f, ORC_MAT_CARPET);
+  orc_agent* ag = orc_agent_create(h, seed);
+  float* S = (float*)malloc(sizeof(float) * 12 * T);
+  float* Ac = (float*)malloc(sizeof(float) * 4 * T);
+  float* Lp = (float*)malloc(sizeof(float) * 4 * T);
+  float* R = (float*)malloc(sizeof(float) * T);
+  float state[12];
+  orc_env_get_obs(env, state);
+  for (int t = 0; t < T; t++) {
+    memcpy(S + 12 * t, state, sizeof(state));
+    orc_sample_actions(ag, state, seed, 0, (uint32_t)t, Ac + 4 * t, Lp + 4 * t);
+    int done;
+    orc_env_step(env, Ac + 4 * t, state, &R[t], &done, NULL);
+  }
+  const double t0 = now_s();
+  orc_train_trajectory(ag, h, seed, 0, T, S, Ac, Lp, R);
+  const double dt = now_s() - t0;
+  free(S); free(Ac); free(Lp); free(R);
+  orc_agent_destroy(ag);
+  orc_env_destroy(env);
+  return dt;
 }

@@ -165,6 +165,12 @@ void orc_normalize(int n, float* x, float eps_clip);
 /* single-walker reference loop (Game1.Update x n_steps, Train at each terminal):
  * the CPU baseline workload.  Returns episodes completed. */
 int orc_reference_loop(const orc_hyper* h, uint64_t seed, int n_steps, double* train_seconds);
+int orc_reference_loop_env(const orc_hyper* h, uint64_t seed, int env_id, int n_steps,
+                           double* train_seconds);
+void orc_train_trajectory(orc_agent* ag, const orc_hyper* h, uint64_t seed, uint32_t update, int T,
+                          const float* S, const float* Ac, const float* Lp, const float* R);
+int orc_physics_loop(const orc_hyper* h, uint64_t seed, int env_id, int n_steps);
+double orc_train_episode_seconds(const orc_hyper* h, uint64_t seed, int T);
 
 #ifdef __cplusplus
 }
