@@ -370,7 +370,7 @@ def main():
             "flop_per_env_step_counted": f_counted,
             "flop_per_env_step_upper_bound": FLOP_UPPER,
             "events_per_env_step": {k: v / ev["env_steps"] for k, v in ev.items()
-                                    if not k.startswith("r1") and k != "env_steps"},
+                                    if k != "env_steps"},
             "hbm_GBs": (traffic / (launch_ms * 1e-3) / 1e9) if traffic else None,
             "hbm_frac": (traffic / (launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBS) if traffic else None,
             "alg_bytes_per_launch": alg_bytes,

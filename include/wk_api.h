@@ -382,7 +382,8 @@ int wk_profile_reset(wk_ctx* ctx);
  * bounding-box hits leg-leg / leg-floor / torso-floor (each runs SAT); SAT collisions
  * (contacts + MoveObjects) in the same three classes; contact resolutions with >= 1 point
  * (the impulse pair) in the same three classes; contact points; walker-substeps; env-steps;
- * auto-resets; 2 reserved. */
+ * auto-resets; walker env-steps with >= 1 leg-floor bounding-box hit; walker env-steps with
+ * >= 1 leg-leg SAT collision. */
 #define WK_NEV 16
 int wk_count_events(wk_ctx* ctx, int k, uint64_t* counts);
 

@@ -117,6 +117,8 @@ def lib():
             "orc_reference_loop": (I, [C.POINTER(Hyper), U64, I, C.POINTER(C.c_double)]),
             "orc_reference_loop_env": (I, [C.POINTER(Hyper), U64, I, I, C.POINTER(C.c_double)]),
             "orc_physics_loop": (I, [C.POINTER(Hyper), U64, I, I]),
+            "orc_train_trajectory": (None, [C.c_void_p, C.POINTER(Hyper), U64, C.c_uint32, I, C.c_void_p,
+                                            C.c_void_p, C.c_void_p, C.c_void_p]),
             "orc_train_episode_seconds": (C.c_double, [C.POINTER(Hyper), U64, I]),
         }
         for name, (res, args) in sig.items():
@@ -263,6 +265,16 @@ class Agent:
         lp = np.empty(4, np.float32)
         lib().orc_sample_actions(self.p, _p(s), int(seed), int(env), int(t), _p(a), _p(lp))
         return a, lp
+
+    def train_trajectory(self, states, actions, logp, rewards, seed, update):
+        """PPOAgent.Train(Trajectory) on one T-step episode (returns, Epochs x floor(T/BatchSize)
+        keyed minibatches, Adam after each)"""
+        S = np.ascontiguousarray(states, np.float32)
+        A = np.ascontiguousarray(actions, np.float32)
+        L = np.ascontiguousarray(logp, np.float32)
+        R = np.ascontiguousarray(rewards, np.float32)
+        lib().orc_train_trajectory(self.p, C.byref(self.h), int(seed), int(update), int(R.size),
+                                   _p(S), _p(A), _p(L), _p(R))
 
     def train_batch(self, states, actions, logp_old, returns, adv, b_div=None, apply_adam=True):
         s = np.ascontiguousarray(states, np.float32)

@@ -32,6 +32,8 @@ enum : int {
   EV_CONTACTS,                             // contact points found
   EV_SUBSTEPS,                             // walker-substeps
   EV_ENV_STEPS, EV_RESETS,                 // env-steps, auto-resets
+  EV_STEPS_LF, EV_STEPS_SATLL,             // walker env-steps with >= 1 leg-floor AABB hit /
+                                           // >= 1 leg-leg SAT hit (how concentrated they are)
   NEV = 16                                 // (LL leg-leg, LF leg-floor, BF torso-floor)
 };
 

@@ -644,6 +644,7 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArg
       c = ac[3] - s.torque[3]; s.torque[3] = ac[3]; s.drll.w = s.drll.w + c * 5.0f;
     }
     // StepObjects
+    const uint32_t lf0 = ecnt[EV_AABB_LF], ll0 = ecnt[EV_SAT_LL];
 #pragma unroll 1
     for (int it = 0; it < P.iterations; it++) {
       PairTraceDev* tr = nullptr;
@@ -654,7 +655,11 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArg
       }
       substep<TRACE, L, ROUGH>(s, mp, mb, dt, adx, ady, tr, sub, ter, ec);
     }
-    if (COUNT) ecnt[EV_ENV_STEPS]++;
+    if (COUNT) {
+      ecnt[EV_ENV_STEPS]++;
+      ecnt[EV_STEPS_LF] += ecnt[EV_AABB_LF] != lf0 ? 1u : 0u;
+      ecnt[EV_STEPS_SATLL] += ecnt[EV_SAT_LL] != ll0 ? 1u : 0u;
+    }
     // Walker.Update
     s.prevx = s.posx; s.prevy = s.posy;
     s.posx = s.body.cx; s.posy = s.body.cy;

@@ -19,7 +19,7 @@ NPARAM_CRITIC = 897
 NPAIRS = 9
 NEV = 16  # WK_NEV event counters (wk_count_events)
 EVENTS = ["joint", "aabb_ll", "aabb_lf", "aabb_bf", "sat_ll", "sat_lf", "sat_bf", "imp_ll",
-          "imp_lf", "imp_bf", "contacts", "substeps", "env_steps", "resets", "r14", "r15"]
+          "imp_lf", "imp_bf", "contacts", "substeps", "env_steps", "resets", "steps_lf", "steps_satll"]
 ST_TORQUE, ST_POS, ST_PREV, ST_STEPS, ST_POSTRESET, ST_TERMINAL, ST_EPISODES = (
     100, 104, 106, 108, 109, 110, 111)
 MATERIALS = {"Carpet": 0, "Ice": 1, "Rubber": 2, "Metal": 3, "Wood": 4, "Paper": 5,

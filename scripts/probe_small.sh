@@ -1,3 +1,6 @@
+#!/bin/bash
+# rollout / PPO-update timings at the small per-GPU shapes (BASELINE configs 2-4: 4,096 and
+# 8,192 walkers) for every physics mapping
 set -u
 mkdir -p gpurun_out
 timeout -k 10 300 python scripts/phys_bench.py 8192 64 1 2 16 > gpurun_out/probe_8192.log 2>&1 || exit $?

@@ -80,6 +80,8 @@ def test_count_events_match_oracle_bookkeeping(wk, orc):
         for t in range(T):
             _, _, d, trc = e.step(tr["actions"][t, i], trace=True)
             ref["joint"] += int((trc["joint_depth"] != 0).sum())
+            ref["steps_lf"] += int(trc["aabb_hit"][:, LF].any())
+            ref["steps_satll"] += int(trc["sat_hit"][:, LL].any())
             for cls, slots in (("ll", LL), ("lf", LF), ("bf", BF)):
                 ref["aabb_" + cls] += int(trc["aabb_hit"][:, slots].sum())
                 ref["sat_" + cls] += int(trc["sat_hit"][:, slots].sum())
