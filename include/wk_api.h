@@ -364,6 +364,13 @@ int wk_write_data_file(const char* path, const float* total_rewards, int64_t n_r
 int wk_comm_unique_id(uint8_t* id /* 128 bytes */);
 int wk_comm_init(wk_ctx* ctx, int rank, int nranks, const uint8_t* unique_id);
 int wk_allreduce_test(wk_ctx* ctx, float* host_buf, int n); /* sum in place (tests) */
+/* The same minibatch sequence with a caller-supplied all-reduce instead of RCCL: after the
+ * ordered reduction each minibatch's slab (gradient + diagnostics, n floats) is copied to the
+ * host, fn must replace it in place with the sum over ranks (return 0), and it is copied back
+ * before Adam.  For hosts without RCCL (MPI, a CPU control plane) and for testing the
+ * multi-rank path of several processes sharing one GPU (RCCL refuses duplicate devices). */
+typedef int (*wk_host_allreduce_fn)(float* buf, int n, void* user);
+int wk_comm_init_host(wk_ctx* ctx, int rank, int nranks, wk_host_allreduce_fn fn, void* user);
 
 /* profiling */
 /* level 0 off; 1: HIP events around each rollout / returns pass / whole PPO update (cheap

@@ -84,6 +84,9 @@ struct wk_ctx {
   // comm
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
+  wk_host_allreduce_fn host_ar = nullptr;  // wk_comm_init_host: a caller-supplied all-reduce
+  void* host_ar_user = nullptr;
+  std::vector<float> host_ar_buf;
   // profiling
   int prof = 0;  // profile level
   struct Ev { int kind; hipEvent_t a, b; int64_t units; };
@@ -989,7 +992,7 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   float* part2 = c->partial + (size_t)nblocks * wk::SLAB;
   // with a communicator (any size, also one rank) the collective path runs: reduction,
   // RCCL all-reduce, Adam -- a single-GPU test then covers the multi-GPU sequence
-  const bool multi = c->comm != nullptr;
+  const bool multi = c->comm != nullptr || c->host_ar != nullptr;
   if (apply_adam && !multi) {  // one GPU: the last reduction stage applies Adam
     ProfScope ps(c, PK_REDUCE, 0, 2);
     HIPCHK(c, wk::launch_grad_reduce_adam(c->partial, nblocks, part2, c->grad, a, c->stream));
@@ -1001,9 +1004,23 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   }
   if (multi) {
     ProfScope ps(c, PK_ALLRED, 0, 2);
-    ncclResult_t r = ncclAllReduce(c->grad, c->grad, wk::SLAB, ncclFloat, ncclSum,
-                                   c->comm, c->stream);
-    if (r != ncclSuccess) { SETERR(c, "ncclAllReduce: %s", ncclGetErrorString(r)); return WK_ERR_COMM; }
+    if (c->comm) {
+      ncclResult_t r = ncclAllReduce(c->grad, c->grad, wk::SLAB, ncclFloat, ncclSum,
+                                     c->comm, c->stream);
+      if (r != ncclSuccess) { SETERR(c, "ncclAllReduce: %s", ncclGetErrorString(r)); return WK_ERR_COMM; }
+    } else {  // host all-reduce: the slab goes through the caller's function between two copies
+      c->host_ar_buf.resize(wk::SLAB);
+      HIPCHK(c, hipMemcpyAsync(c->host_ar_buf.data(), c->grad, sizeof(float) * wk::SLAB,
+                               hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      if (c->host_ar(c->host_ar_buf.data(), wk::SLAB, c->host_ar_user) != 0) {
+        SETERR(c, "host all-reduce callback failed");
+        return WK_ERR_COMM;
+      }
+      HIPCHK(c, hipMemcpyAsync(c->grad, c->host_ar_buf.data(), sizeof(float) * wk::SLAB,
+                               hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));  // the host buffer is reused next minibatch
+    }
   }
   if (apply_adam) {
     ProfScope ps(c, PK_ADAM, 0, 2);
@@ -1146,11 +1163,23 @@ int wk_comm_unique_id(uint8_t* id) {
 int wk_comm_init(wk_ctx* c, int rank, int nranks, const uint8_t* id) {
   DevGuard dg_(c);
   if (!c || !id || nranks <= 0 || rank < 0 || rank >= nranks) return WK_ERR_ARG;
+  if (c->host_ar) { SETERR(c, "the context already has a host all-reduce"); return WK_ERR_STATE; }
   HIPCHK(c, hipSetDevice(c->device));
   ncclUniqueId u;
   memcpy(&u, id, sizeof(u));
   ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
   if (r != ncclSuccess) { SETERR(c, "ncclCommInitRank: %s", ncclGetErrorString(r)); c->comm = nullptr; return WK_ERR_COMM; }
+  c->rank = rank;
+  c->nranks = nranks;
+  return WK_OK;
+}
+
+int wk_comm_init_host(wk_ctx* c, int rank, int nranks, wk_host_allreduce_fn fn, void* user) {
+  DevGuard dg_(c);
+  if (!c || !fn || nranks <= 0 || rank < 0 || rank >= nranks) return WK_ERR_ARG;
+  if (c->comm) { SETERR(c, "the context already has an RCCL communicator"); return WK_ERR_STATE; }
+  c->host_ar = fn;
+  c->host_ar_user = user;
   c->rank = rank;
   c->nranks = nranks;
   return WK_OK;

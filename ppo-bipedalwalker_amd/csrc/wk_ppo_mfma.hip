@@ -114,6 +114,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
   // ---- stage the weight image (already in operand order, wk_mfma_layout.h): every
   // thread's loads are issued before its first LDS write, so the copy costs one L2
   // round trip instead of one per 4 KB ----
+#ifndef WK_GRAD_NOSTAGE  // probe: no weight staging (fixed-cost measurement)
   {
     constexpr int NV = WEND / 4, PER = (NV + 64 * WAVES - 1) / (64 * WAVES);
     f4 wv[PER];
@@ -128,6 +129,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
       if (e < NV) ((f4*)lds)[e] = wv[i];
     }
   }
+#endif
   float* cb = lds + WEND + wave * CHUNK;
   for (int e = lane; e < 256; e += 64) cb[C_G3 + e] = 0.0f;
   __syncthreads();
@@ -434,6 +436,9 @@ void k_ppo_grad_mfma(GradArgs ga) {
     }
   }
   __syncthreads();
+#ifdef WK_GRAD_NOFOLD  // probe: no block fold
+  if (ga.samples >= 0) return;
+#endif
   float* out = ga.partial + (size_t)blockIdx.x * SLAB;
   for (int i = tid; i < SLAB; i += 64 * WAVES) {
     float acc = 0.0f;

@@ -38,7 +38,7 @@ EXPORTS = [
     "wk_host_settings_defaults", "wk_config_to_json", "wk_config_from_json",
     "wk_config_save_json", "wk_config_load_json", "wk_collect_data", "wk_episode_log_count",
     "wk_episode_log_drain", "wk_loss_log_drain", "wk_write_data_file",
-    "wk_comm_unique_id", "wk_comm_init", "wk_allreduce_test", "wk_profile_enable",
+    "wk_comm_unique_id", "wk_comm_init", "wk_comm_init_host", "wk_allreduce_test", "wk_profile_enable",
     "wk_profile_get", "wk_profile_reset", "wk_count_events", "wk_snapshot",
 ]
 
@@ -153,6 +153,8 @@ class Profile(C.Structure):
 
 
 _lib = None
+# wk_host_allreduce_fn: int (*)(float* buf, int n, void* user)
+HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_float), C.c_int, C.c_void_p)
 
 
 def load_library(path=None):
@@ -229,6 +231,7 @@ def load_library(path=None):
         "wk_comm_unique_id": (I, [P]),
         "wk_comm_init": (I, [P, I, I, P]),
         "wk_allreduce_test": (I, [P, P, I]),
+        "wk_comm_init_host": (I, [P, I, I, HOST_ALLREDUCE_FN, P]),
         "wk_profile_enable": (I, [P, I]),
         "wk_profile_get": (I, [P, C.POINTER(Profile)]),
         "wk_profile_reset": (I, [P]),
@@ -636,6 +639,19 @@ class Engine:
     def comm_init(self, rank, nranks, uid):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         self._chk(self.lib.wk_comm_init(self.h, int(rank), int(nranks), buf), "wk_comm_init")
+
+    def comm_init_host(self, rank, nranks, allreduce):
+        """wk_comm_init_host: `allreduce(np.ndarray float32 view)` sums the slab over ranks in
+        place (e.g. torch.distributed over gloo); the callback object is kept alive here."""
+        def _cb(buf, n, user):
+            try:
+                allreduce(np.ctypeslib.as_array(buf, shape=(n,)))
+                return 0
+            except Exception:  # noqa: BLE001 -- reported as WK_ERR_COMM by the library
+                return 1
+        self._host_ar = HOST_ALLREDUCE_FN(_cb)
+        self._chk(self.lib.wk_comm_init_host(self.h, int(rank), int(nranks), self._host_ar, None),
+                  "wk_comm_init_host")
 
     def allreduce_test(self, x):
         x = _f32(x).copy()

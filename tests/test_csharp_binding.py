@@ -43,7 +43,7 @@ def cs_imports():
 
 def c_kind(p):
     """the marshalling class of one C parameter"""
-    if "*" in p:
+    if "*" in p or p.startswith("wk_host_allreduce_fn"):
         return "ptr"
     t = p.split()[0:-1]
     t = " ".join(t)
@@ -57,7 +57,7 @@ def cs_kind(p):
     if toks[0] in ("ref", "out"):
         return "ptr"
     t = toks[0]
-    if t.endswith("[]") or t.endswith("[]?") or t in ("IntPtr", "string"):
+    if t.endswith("[]") or t.endswith("[]?") or t in ("IntPtr", "string", "HostAllReduce"):
         return "ptr"
     return {"int": "i32", "uint": "u32", "ulong": "u64", "long": "i64", "float": "f32",
             "UIntPtr": "usize"}[t]

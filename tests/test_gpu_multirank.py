@@ -1,0 +1,76 @@
+"""GPU, two processes sharing GPU 0: libwk's multi-rank minibatch sequence.
+
+RCCL refuses two ranks on one device, so the ranks' all-reduce goes through
+wk_comm_init_host (the same sequence: ordered block reduction -> all-reduce of the 6,153-float
+slab -> replicated Adam) with torch.distributed over gloo.  Each rank holds its contiguous
+shard of the walkers (EnvOffset = rank x 256) and the global minibatch divisor; checked:
+
+  * each rank's rollout equals a communicator-free context on the same shard (sharding by
+    EnvOffset: Philox streams keyed by the global walker id);
+  * after one minibatch the all-reduced update is exactly Adam(t = 1) of the SUM of the two
+    ranks' local gradients (each recomputed by the same kernel on the same permuted samples,
+    divisor = global minibatch), bit for bit in float32 -- the sum the RCCL all-reduce forms;
+  * the diagnostics are the sums of the ranks' local diagnostics;
+  * the two replicas' weights and Adam state stay bit-identical through a second iteration.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _adam_t1(w, g, alpha=np.float32(0.001), beta1=0.9, beta2=0.999, eps=np.float32(1e-8)):
+    """DenseLayer.Adam at t = 1 from zero moments, op for op as adam_param (wk_ppo.hip)"""
+    f = np.float32
+    c1, c2 = f(1.0) - f(beta1), f(1.0) - f(beta2)
+    bc1 = f(1.0 - np.float64(f(beta1)) ** 1)
+    bc2 = f(1.0 - np.float64(f(beta2)) ** 1)
+    m = (g * c1) + (np.zeros_like(g) * f(beta1))
+    v = (np.zeros_like(g) * f(beta2)) + ((g * g) * c2)
+    mh = m / bc1
+    vh = v / bc2
+    den = np.sqrt(vh) + eps
+    return w - ((mh / den) * alpha), m, v
+
+
+def test_two_ranks_host_allreduce(tmp_path):
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(
+            ["timeout", "-k", "10", "240", sys.executable,
+             os.path.join(ROOT, "tests", "workers", "multirank_worker.py"), str(tmp_path)],
+            env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate()[0] for p in procs]
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-3000:]
+    r0, r1 = (np.load(tmp_path / f"rank{r}.npz") for r in range(2))
+    for r in (r0, r1):
+        assert r["same_traj"] and r["same_state"]
+    np.testing.assert_array_equal(r0["w0"], r1["w0"])
+    g_sum = r0["g_local"] + r1["g_local"]
+    w_ref, m_ref, v_ref = _adam_t1(r0["w0"], g_sum)
+    for r in (r0, r1):
+        np.testing.assert_array_equal(r["w1"], w_ref)
+        np.testing.assert_array_equal(r["m1"], m_ref)
+        np.testing.assert_array_equal(r["v1"], v_ref)
+        assert int(r["t1"]) == 1
+        assert float(r["cd"]) == np.float32(r0["cd_l"]) + np.float32(r1["cd_l"])
+        assert float(r["ad"]) == np.float32(r0["ad_l"]) + np.float32(r1["ad_l"])
+    np.testing.assert_array_equal(r0["w2"], r1["w2"])
+    assert not np.array_equal(r0["state"], r1["state"])  # different shards

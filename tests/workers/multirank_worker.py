@@ -1,0 +1,64 @@
+"""One rank of tests/test_gpu_multirank.py: RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT from
+the environment, gloo control plane, a libwk context on GPU 0 whose minibatch all-reduce goes
+through wk_comm_init_host -> torch.distributed.all_reduce (RCCL refuses two ranks on one
+device).  Writes its results to <out>/rank<r>.npz."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "ppo-bipedalwalker_amd"))
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import wk  # noqa: E402
+from wk.dist import env_from_launcher, make_shard  # noqa: E402
+
+SEED = 20250905
+out_dir = sys.argv[1]
+n_local, T = 256, 8
+rank, world, _ = env_from_launcher()
+dist.init_process_group("gloo")
+shard = make_shard(rank, world, 0, n_local, n_local * T)  # one minibatch = the local pool
+cfg = dict(Horizon=T, Minibatch=shard.minibatch_local, MinibatchGlobal=shard.minibatch_global,
+           EnvOffset=shard.env_offset, RandomizeStart=1, RandomizeMaterial=1, Epochs=1)
+
+
+def allreduce(a):
+    t = torch.from_numpy(a)  # shares the slab's memory
+    dist.all_reduce(t)       # gloo sum over the ranks, in place
+
+
+eng = wk.Engine(n_local, seed=SEED, **cfg)
+solo = wk.Engine(n_local, seed=SEED, **cfg)  # same shard, no communicator
+eng.comm_init_host(rank, world, allreduce)
+w0 = eng.get_weights()
+eng.rollout(T)
+solo.rollout(T)
+tr = eng.get_trajectory(T)
+tr_solo = solo.get_trajectory(T)
+same_traj = all(np.array_equal(tr[k], tr_solo[k]) for k in tr)
+same_state = np.array_equal(eng.get_state(), solo.get_state())
+cd, ad = eng.ppo_update(update_index=0)
+# this rank's local gradient of the same (only) minibatch, recomputed by the same kernel
+pool = n_local * T
+key = None
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import orc  # noqa: E402  (checker: the permutation the engine draws its minibatch with)
+key = orc.perm_key(SEED, 0, 0)
+idx = np.array([orc.perm(i, pool, key) for i in range(pool)])
+flat = lambda x, d: x.reshape(pool, d) if d > 1 else x.reshape(pool)
+g_local, cd_l, ad_l, sk = solo.minibatch_gradient(
+    flat(tr["states"], 12)[idx], flat(tr["actions"], 4)[idx], flat(tr["logp"], 4)[idx],
+    flat(tr["returns"], 1)[idx], flat(tr["advantages"], 1)[idx], b_div=shard.minibatch_global)
+w1 = eng.get_weights()
+m1, v1, t1 = eng.get_adam()
+eng.rollout(T)  # a second iteration: the replicas stay identical
+eng.ppo_update(update_index=1)
+w2 = eng.get_weights()
+np.savez(os.path.join(out_dir, f"rank{rank}.npz"), w0=w0, w1=w1, m1=m1, v1=v1, t1=t1, w2=w2,
+         g_local=g_local, cd=cd, ad=ad, cd_l=cd_l, ad_l=ad_l, same_traj=same_traj,
+         same_state=same_state, state=eng.get_state())
+eng.close()
+solo.close()
+dist.destroy_process_group()
