@@ -100,7 +100,10 @@ struct AdamArgs {
   float c1, c2, beta1, beta2, bc1, bc2, alpha, eps;
 };
 
-enum : int { SLAB = NPARAM + 4 };  // gradient + critic diag, actor diag, skipped, pad
+// gradient + critic diag, actor diag, skipped, then zero pads to a multiple of 4 floats (16-byte
+// rows: the matrix-core kernel's block fold and slab stores are f4-wide)
+enum : int { SLAB = (NPARAM + 3 + 3) / 4 * 4 };
+static_assert(SLAB % 4 == 0 && SLAB >= NPARAM + 3, "slab layout");
 
 hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s);
 hipError_t launch_env_scene(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,

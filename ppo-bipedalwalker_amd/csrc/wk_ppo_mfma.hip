@@ -79,12 +79,26 @@ DEV float row_sum16(float v) {
   return v;
 }
 
+// Optional phase profile (build with -DWK_GRAD_PROF; scripts/grad_prof.py): wave 0 of each block
+// accumulates s_memtime deltas per phase, summed over blocks into g_grad_prof.
+#ifdef WK_GRAD_PROF
+__device__ unsigned long long g_grad_prof[16];
+#define GP_MARK(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); gp[k] += t_ - gp_t; gp_t = t_; } while (0)
+#define GP_FLUSH() do { if (tid == 0) for (int k_ = 0; k_ < 12; k_++) atomicAdd(&g_grad_prof[k_], (unsigned long long)gp[k_]); } while (0)
+#else
+#define GP_MARK(k) do {} while (0)
+#define GP_FLUSH() do {} while (0)
+#endif
+
 __global__ __launch_bounds__(64 * mf::WAVES) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_ppo_grad_mfma(GradArgs ga) {
   using namespace mf;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, g = lane >> 4;
+#ifdef WK_GRAD_PROF
+  uint64_t gp[12] = {}, gp_t = __builtin_amdgcn_s_memtime();
+#endif
 
 #ifdef WK_GRAD_NOLOOP  // probe: the launch without its chunk loop (fixed-cost measurement)
   const int nchunks = 0;
@@ -169,6 +183,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
 #pragma unroll
     for (int d = 0; d < 4; d++) w3[d][Mt] = *(const f4*)(lds + W3 + d * 64 + 16 * Mt + 4 * g);
   }
+  GP_MARK(0);  // prologue
 #pragma unroll 1
   for (; c < nchunks; c += nw) {
     const Smp cur = nxt;
@@ -182,53 +197,67 @@ void k_ppo_grad_mfma(GradArgs ga) {
     }
     wave_sync();
 
+    GP_MARK(1);  // gather issue + SX tile
+#ifdef WK_PROBE_EMPTY  // probe: the loop body reduced to the gather and a token accumulation
+    db3 += cb[C_SX + sx(n, g)] + act + lpo + ret + adv;
+    (void)valid;
+    continue;
+#endif
     // ---- layer 1, actor and critic ----
     float sB[3];
 #pragma unroll
     for (int t = 0; t < 3; t++) sB[t] = cb[C_SX + sx(n, 4 * t + g)];
+    // (the 8 accumulators' MFMAs interleaved: a dependent v_mfma_f32_16x16x4_f32 waits 40
+    // cycles, an independent one issues after 32; the bias / activation VALU after the last)
     f4 z1[4], zc1[4], h1[4], hc1[4];
 #pragma unroll
-    for (int Mt = 0; Mt < 4; Mt++) {
-      f4 acc = z4, accc = z4;
+    for (int Mt = 0; Mt < 4; Mt++) { z1[Mt] = z4; zc1[Mt] = z4; }
 #pragma unroll
-      for (int t = 0; t < 3; t++) {
-        acc = mfma(wa1[Mt][t], sB[t], acc);
-        accc = mfma(wc1[Mt][t], sB[t], accc);
+    for (int t = 0; t < 3; t++)
+#pragma unroll
+      for (int Mt = 0; Mt < 4; Mt++) {
+        z1[Mt] = mfma(wa1[Mt][t], sB[t], z1[Mt]);
+        zc1[Mt] = mfma(wc1[Mt][t], sB[t], zc1[Mt]);
       }
+#pragma unroll
+    for (int Mt = 0; Mt < 4; Mt++) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        acc[r] = acc[r] + ba1[Mt][r];
-        accc[r] = accc[r] + bc1[Mt][r];
-        h1[Mt][r] = mf_lrelu(acc[r]);
-        hc1[Mt][r] = mf_lrelu(accc[r]);
+        z1[Mt][r] = z1[Mt][r] + ba1[Mt][r];
+        zc1[Mt][r] = zc1[Mt][r] + bc1[Mt][r];
+        h1[Mt][r] = mf_lrelu(z1[Mt][r]);
+        hc1[Mt][r] = mf_lrelu(zc1[Mt][r]);
       }
-      z1[Mt] = acc;
-      zc1[Mt] = accc;
       *(f4*)(cb + C_H1 + tw(n, 16 * Mt + 4 * g)) = h1[Mt];
       *(f4*)(cb + C_HC1 + tw(n, 16 * Mt + 4 * g)) = hc1[Mt];
     }
+    GP_MARK(2);  // layer 1
     // ---- layer 2 (B operand = layer 1's D registers) ----
     f4 w2[4][4];
 #pragma unroll
     for (int Mt = 0; Mt < 4; Mt++)
 #pragma unroll
       for (int Mp = 0; Mp < 4; Mp++) w2[Mt][Mp] = *(const f4*)(lds + W2F + ((Mt * 4 + Mp) * 64 + lane) * 4);
+    // (four chains interleaved, each accumulator's k order (Mp, r) unchanged)
     f4 z2[4], h2[4];
 #pragma unroll
+    for (int Mt = 0; Mt < 4; Mt++) z2[Mt] = z4;
+#pragma unroll
+    for (int Mp = 0; Mp < 4; Mp++)
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int Mt = 0; Mt < 4; Mt++) z2[Mt] = mfma(w2[Mt][Mp][r], h1[Mp][r], z2[Mt]);
+#pragma unroll
     for (int Mt = 0; Mt < 4; Mt++) {
-      f4 acc = z4;
-#pragma unroll
-      for (int Mp = 0; Mp < 4; Mp++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) acc = mfma(w2[Mt][Mp][r], h1[Mp][r], acc);
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        acc[r] = acc[r] + ba2[Mt][r];
-        h2[Mt][r] = mf_lrelu(acc[r]);
+        z2[Mt][r] = z2[Mt][r] + ba2[Mt][r];
+        h2[Mt][r] = mf_lrelu(z2[Mt][r]);
       }
-      z2[Mt] = acc;
       *(f4*)(cb + C_H2 + tw(n, 16 * Mt + 4 * g)) = h2[Mt];
     }
+    GP_MARK(3);  // layer 2
     // ---- output rows: actor z3[0..3] on h2, critic V on hc1 ----
     float p3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, pv = 0.0f;
 #pragma unroll
@@ -250,6 +279,20 @@ void k_ppo_grad_mfma(GradArgs ga) {
     const float z3 = (g == 0 ? p3[0] : g == 1 ? p3[1] : g == 2 ? p3[2] : p3[3]) + b3g;
     const float V = pv + bc2;
 
+    GP_MARK(4);  // output rows
+#ifdef WK_PROBE_NOLOSS
+    const bool use = valid;
+    float criticLoss = use ? (V - ret) * 1e-3f : 0.0f;
+    float actorLoss = use ? (z3 - act) * 1e-3f : 0.0f;
+    const float gz3 = actorLoss;
+    float al[4], q[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      al[d] = __shfl(actorLoss, n + 16 * d);
+      q[d] = __shfl(gz3, n + 16 * d);
+    }
+    (void)lpo; (void)adv;
+#else
     // ---- PPO derivative for action dimension d = g (PPOAgent.cs:234-326) ----
     const float mean = tanhf(z3);
     float criticLoss = 2.0f * (V - ret);
@@ -284,6 +327,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
       al[d] = __shfl(actorLoss, n + 16 * d);
       q[d] = __shfl(gz3, n + 16 * d);
     }
+#endif
     if (g == 0) {
       diagC += criticLoss;
       diagA += use ? ((((0.0f + al[0]) + al[1]) + al[2]) + al[3]) / 4.0f : 0.0f;
@@ -293,6 +337,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
     }
     db3 += gz3;
     cb[C_G3 + sx(n, g)] = gz3;
+    GP_MARK(5);  // loss
     // ---- gh2 = W3^T gz3 -> gz2; critic gzc1 = (Wc2 dV) * lrelu'(zc1) ----
     f4 gz2[4], gzc1[4];
 #pragma unroll
@@ -310,7 +355,11 @@ void k_ppo_grad_mfma(GradArgs ga) {
       *(f4*)(cb + C_G2 + tw(n, 16 * Mt + 4 * g)) = gz2[Mt];
     }
     wave_sync();
+    GP_MARK(6);  // gz2 / gzc1 + G2 tile
     // ---- dW3 | dWc2 += [gz3; dV]^T [H2 | Hc1]; dW2 += gz2^T H1 (samples on K) ----
+#ifdef WK_PROBE_NOBWD
+    if (ga.samples < 0)
+#endif
     {
       float av[4], bv[4][8], ag[4][4], bh[4][4];
 #pragma unroll
@@ -339,26 +388,40 @@ void k_ppo_grad_mfma(GradArgs ga) {
       }
     }
     wave_sync();  // H2 / Hc1 reads done before G1 / Gc1 overwrite them
+    GP_MARK(7);  // dW3 / dW2
     // ---- gh1^T = W2^T gz2^T (B = gz2 registers) -> gz1 ----
+#ifdef WK_PROBE_NOBWD
+    if (ga.samples < 0)
+#endif
+    {
 #pragma unroll
     for (int Mk = 0; Mk < 4; Mk++)
 #pragma unroll
       for (int Mj = 0; Mj < 4; Mj++) w2[Mk][Mj] = *(const f4*)(lds + W2B + ((Mk * 4 + Mj) * 64 + lane) * 4);
+    f4 gh1[4];  // (four chains interleaved)
+#pragma unroll
+    for (int Mk = 0; Mk < 4; Mk++) gh1[Mk] = z4;
+#pragma unroll
+    for (int Mj = 0; Mj < 4; Mj++)
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int Mk = 0; Mk < 4; Mk++) gh1[Mk] = mfma(w2[Mk][Mj][r], gz2[Mj][r], gh1[Mk]);
 #pragma unroll
     for (int Mk = 0; Mk < 4; Mk++) {
-      f4 acc = z4;
-#pragma unroll
-      for (int Mj = 0; Mj < 4; Mj++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) acc = mfma(w2[Mk][Mj][r], gz2[Mj][r], acc);
       f4 gz1;
 #pragma unroll
-      for (int r = 0; r < 4; r++) gz1[r] = acc[r] * mf_dlrelu(z1[Mk][r]);
+      for (int r = 0; r < 4; r++) gz1[r] = gh1[Mk][r] * mf_dlrelu(z1[Mk][r]);
       *(f4*)(cb + C_G1 + tw(n, 16 * Mk + 4 * g)) = gz1;
       *(f4*)(cb + C_GC1 + tw(n, 16 * Mk + 4 * g)) = gzc1[Mk];
     }
+    }
     wave_sync();
+    GP_MARK(8);  // gh1 + gz1
     // ---- dW1 | db1, dWc1 | dbc1 += gz1^T [S | 1] ----
+#ifdef WK_PROBE_NOBWD
+    if (ga.samples < 0)
+#endif
     {
       float bx[4], a1v[4][4], a1cv[4][4];
 #pragma unroll
@@ -380,11 +443,13 @@ void k_ppo_grad_mfma(GradArgs ga) {
         }
     }
     wave_sync();  // the next chunk rewrites every tile
+    GP_MARK(9);  // dW1
   }
 
 #ifdef WK_GRAD_NOEPI  // probe: no epilogue
   if (ga.samples >= 0) return;
 #endif
+  GP_MARK(10);  // (loop exit)
   // ---- per-lane sums over the 16 sample lanes of each row ----
 #pragma unroll
   for (int i = 0; i < 16; i++) db2[i] = row_sum16(db2[i]);
@@ -397,7 +462,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
   // ---- each wave writes its slab, then the block sums them in wave order ----
   __syncthreads();  // every wave is done with the weights and tiles
   float* slab = lds + wave * SLAB;  // every entry below is written exactly once
-  if (lane == 0) slab[NPARAM + 3] = 0.0f;  // (the pad)
+  if (lane < SLAB - (NPARAM + 3)) slab[NPARAM + 3 + lane] = 0.0f;  // (the pads)
 #pragma unroll
   for (int Mj = 0; Mj < 4; Mj++)
 #pragma unroll
@@ -439,13 +504,27 @@ void k_ppo_grad_mfma(GradArgs ga) {
 #ifdef WK_GRAD_NOFOLD  // probe: no block fold
   if (ga.samples >= 0) return;
 #endif
-  float* out = ga.partial + (size_t)blockIdx.x * SLAB;
-  for (int i = tid; i < SLAB; i += 64 * WAVES) {
-    float acc = 0.0f;
+  // the block fold, 16 bytes per lane and step with every LDS read of a lane issued up front
+  // (same element order: ((0 + w0) + w1) + w2) + w3)
+  f4* out = (f4*)(ga.partial + (size_t)blockIdx.x * SLAB);
+  constexpr int NV = SLAB / 4, PER = (NV + 64 * WAVES - 1) / (64 * WAVES);
+  f4 sv[PER][WAVES];
 #pragma unroll
-    for (int w = 0; w < WAVES; w++) acc = acc + lds[w * SLAB + i];
-    out[i] = acc;
+  for (int k = 0; k < PER; k++) {
+    const int i = tid + k * 64 * WAVES;
+#pragma unroll
+    for (int w = 0; w < WAVES; w++) sv[k][w] = i < NV ? ((const f4*)(lds + w * SLAB))[i] : z4;
   }
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int i = tid + k * 64 * WAVES;
+    f4 acc = z4;
+#pragma unroll
+    for (int w = 0; w < WAVES; w++) acc = acc + sv[k][w];
+    if (i < NV) out[i] = acc;
+  }
+  GP_MARK(11);
+  GP_FLUSH();
 }
 
 // the weight image from the flat parameters (initialisation, wk_set_weights)
@@ -455,6 +534,16 @@ __global__ void k_swizzle(const float* __restrict__ W, float* __restrict__ Wz) {
 }
 
 int mfma_image_floats() { return mf::WEND; }
+#ifdef WK_GRAD_PROF
+extern "C" int wk_grad_prof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_grad_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_grad_prof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 hipError_t launch_swizzle(const float* W, float* Wz, hipStream_t s) {
   hipLaunchKernelGGL(k_swizzle, dim3((NPARAM + 255) / 256), dim3(256), 0, s, W, Wz);
   return hipGetLastError();
