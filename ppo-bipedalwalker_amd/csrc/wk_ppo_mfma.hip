@@ -527,6 +527,456 @@ void k_ppo_grad_mfma(GradArgs ga) {
   GP_FLUSH();
 }
 
+// ---------------------------------------------------------------------------------------
+// k_ppo_grad_ws: the same minibatch gradient with two waves per SIMD in producer / consumer
+// roles (8-wave blocks; waves p and p + 4 form pair p, one SIMD).  One wave per SIMD leaves
+// the matrix core idle while the single wave runs its loss / activation VALU chain and waits
+// on dependencies (k_ppo_grad_mfma: 40 % MFMA-busy, 40 % of wave cycles in dependency waits,
+// profiles/r02_pmc_grad_sq_issue.csv).  Here the producer runs the forward pass, the loss and
+// the VALU-side gradients of chunk k (layer 1 and 2: 88 MFMAs) while its partner runs the
+// matrix-core backward of chunk k - 1 (dW2, gh1, dW1, dWc1: 160 MFMAs), so the SIMD always
+// has independent work from the other wave; one block barrier per chunk step hands the
+// chunk's tiles over (double-buffered).
+//   producer: gather, Z1 / Zc1 / Z2 (N layout), z3, V, the loss, gz3, dV;
+//             dW3 += gz3^T H2, dWc2 += dV^T Hc1 (VALU FMAs into per-lane partials),
+//             db2 / db3 / dbc2 / diagnostics; tiles H1, G2 = gz2, GC1 = gzc1, SX = [S | 1]
+//   consumer: gh1^T = W2^T gz2^T (B = gz2 read back in N layout), gz1 = gh1 * lrelu'(h1),
+//             dW2 += gz2^T H1, then G1 (into the consumed H1 buffer), dW1 | db1 += gz1^T
+//             [S | 1], dWc1 | dbc1 += gzc1^T [S | 1]
+// Tiles [16 samples][68] (4 rows = 16 banks apart) and SX [16][20]: every access below is
+// bank-conflict-free; the sample contractions take K step r = samples 4 g + r.  A pair's
+// producer and consumer own disjoint parameters, so they write one slab and the block folds
+// the four pair slabs in pair order (ordered reduction as before).
+#ifndef WK_GRAD_PRIO
+#define WK_GRAD_PRIO 2
+#endif
+namespace ws {
+enum : int {
+  RT = 68, T68 = 16 * RT, RSX = 20, TSX = 16 * RSX,
+  O_SX = 0, O_H1 = TSX, O_G2 = O_H1 + T68, O_GC1 = O_G2 + T68, TB = O_GC1 + T68,
+  PAIRS = 4,
+  LOOP_FLOATS = mf::WEND + PAIRS * 2 * TB,
+  LDS_FLOATS = LOOP_FLOATS > PAIRS * SLAB ? LOOP_FLOATS : PAIRS * SLAB
+};
+static_assert(LOOP_FLOATS * 4 <= 160 * 1024, "fits the CU's LDS");
+static_assert(TB % 4 == 0 && T68 % 4 == 0 && TSX % 4 == 0, "16-byte aligned tiles");
+}  // namespace ws
+
+__global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga) {
+  using namespace mf;
+  using namespace ws;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, g = lane >> 4;
+  // Pairs by SIMD: the two waves that share a SIMD (HW_ID.SIMD_ID) become its producer and
+  // consumer, so each SIMD holds one wave of each role whatever the wave placement; if the
+  // eight waves do not sit two per SIMD, pair p = waves p and p + 4.  (The role is
+  // wave-uniform in an SGPR: scalar branches, so each wave executes only its own path's
+  // barriers -- both paths execute the same number.)
+  __shared__ int simd_of[2 * PAIRS];
+  if (lane == 0) simd_of[wave] = (int)((__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4) >> 0) & 3);
+  __syncthreads();
+  int pair = wave & 3;
+  bool producer = wave < PAIRS;
+  {
+    int cnt[PAIRS] = {0, 0, 0, 0}, first[PAIRS] = {-1, -1, -1, -1};
+#pragma unroll
+    for (int w = 0; w < 2 * PAIRS; w++) {
+      const int sm = simd_of[w];
+#pragma unroll
+      for (int q = 0; q < PAIRS; q++) {
+        cnt[q] += sm == q ? 1 : 0;
+        first[q] = (sm == q && first[q] < 0) ? w : first[q];
+      }
+    }
+    bool two_each = true;
+#pragma unroll
+    for (int q = 0; q < PAIRS; q++) two_each = two_each && cnt[q] == 2;
+    if (two_each) {
+      pair = simd_of[wave];
+      producer = first[pair] == wave;
+    }
+  }
+  pair = __builtin_amdgcn_readfirstlane(pair);
+  producer = __builtin_amdgcn_readfirstlane(producer ? 1 : 0) != 0;
+  const int nchunks = (ga.samples + 15) / 16;
+  const int nw = gridDim.x * PAIRS;
+  const int c0 = blockIdx.x * PAIRS + pair;
+  const int kp = c0 < nchunks ? (nchunks - 1 - c0) / nw + 1 : 0;         // this pair's chunks
+  const int kmax = blockIdx.x * PAIRS < nchunks ? (nchunks - 1 - blockIdx.x * PAIRS) / nw + 1 : 0;
+
+  struct Smp { f4 sv; float act, lpo, ret, adv; };
+  auto gather = [&](int c) {
+    Smp m;
+    const int pos = c * 16 + n;
+    uint32_t idx = ga.base + (uint32_t)(pos < ga.samples ? pos : 0);
+    if (ga.use_perm) idx = perm_apply(idx, ga.pk);
+    m.sv = f4{1.0f, 0.0f, 0.0f, 0.0f};  // lane group 3: the bias column
+    if (g < 3) m.sv = *(const f4*)(ga.states + (size_t)idx * 12 + 4 * g);
+    m.act = ga.actions[(size_t)idx * 4 + g];
+    m.lpo = ga.logp_old[(size_t)idx * 4 + g];
+    m.ret = ga.returns[idx];
+    m.adv = ga.adv[idx];
+    return m;
+  };
+  Smp nxt;
+  if (producer) nxt = gather(c0 < nchunks ? c0 : 0);  // in flight while the weights are staged
+  {
+    constexpr int NV = WEND / 4, PER = (NV + 512 - 1) / 512;
+    f4 wv[PER];
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+      const int e = tid + i * 512;
+      if (e < NV) wv[i] = ((const f4*)ga.Wz)[e];
+    }
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+      const int e = tid + i * 512;
+      if (e < NV) ((f4*)lds)[e] = wv[i];
+    }
+  }
+  __syncthreads();
+  float* const pt = lds + WEND + pair * 2 * TB;  // this pair's two tile buffers
+  const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+
+  if (producer) {
+    // ---------------- producer ----------------
+    // (the producer's dependent chain sets the pace: the SIMD's arbiter serves it first, the
+    // consumer's independent MFMAs fill the gaps)
+#if WK_GRAD_PRIO
+    __builtin_amdgcn_s_setprio(WK_GRAD_PRIO);
+#endif
+    f4 aw3[4][4], awc2[4], db2[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      awc2[i] = z4; db2[i] = z4;
+#pragma unroll
+      for (int j = 0; j < 4; j++) aw3[i][j] = z4;
+    }
+    float db3 = 0.0f, dbc2 = 0.0f, diagC = 0.0f, diagA = 0.0f, skipped = 0.0f;
+    const float b3g = lds[BA3 + g], bc2 = lds[BC2];
+    float wa1[4][3], wc1[4][3];
+#pragma unroll
+    for (int M = 0; M < 4; M++)
+#pragma unroll
+      for (int t = 0; t < 3; t++) {
+        wa1[M][t] = lds[AW1F + (M * 3 + t) * 64 + lane];
+        wc1[M][t] = lds[CW1F + (M * 3 + t) * 64 + lane];
+      }
+#pragma unroll 1
+    for (int i = 0; i <= kmax; i++) {
+#ifdef WK_WS_NOPROD  // probe: the consumer alone (on whatever the tiles hold)
+      if (ga.samples < 0)
+#endif
+      if (i < kp) {
+        const int c = c0 + i * nw;
+        float* const tb = pt + (i & 1) * TB;
+        const Smp cur = nxt;
+        if (i + 1 < kp) nxt = gather(c + nw);
+        const bool valid = c * 16 + n < ga.samples;
+        *(f4*)(tb + O_SX + n * RSX + 4 * g) = cur.sv;
+        wave_sync();
+        float sB[3];
+#pragma unroll
+        for (int t = 0; t < 3; t++) sB[t] = tb[O_SX + n * RSX + 4 * t + g];
+        // ---- layer 1, actor and critic (N layout) ----
+        f4 z1[4], zc1[4], h1[4], hc1[4];
+#pragma unroll
+        for (int M = 0; M < 4; M++) { z1[M] = z4; zc1[M] = z4; }
+#pragma unroll
+        for (int t = 0; t < 3; t++)
+#pragma unroll
+          for (int M = 0; M < 4; M++) {
+            z1[M] = mfma(wa1[M][t], sB[t], z1[M]);
+            zc1[M] = mfma(wc1[M][t], sB[t], zc1[M]);
+          }
+#pragma unroll
+        for (int M = 0; M < 4; M++) {
+          const f4 b1 = *(const f4*)(lds + BA1 + 16 * M + 4 * g);
+          const f4 c1 = *(const f4*)(lds + BC1 + 16 * M + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            h1[M][r] = mf_lrelu(z1[M][r] + b1[r]);
+            hc1[M][r] = mf_lrelu(zc1[M][r] + c1[r]);
+          }
+          *(f4*)(tb + O_H1 + n * RT + 16 * M + 4 * g) = h1[M];
+        }
+        // ---- layer 2 (B operand = layer 1's registers) ----
+        f4 z2[4], h2[4];
+#pragma unroll
+        for (int M = 0; M < 4; M++) z2[M] = z4;
+#pragma unroll
+        for (int Mp = 0; Mp < 4; Mp++) {
+          f4 w2[4];
+#pragma unroll
+          for (int M = 0; M < 4; M++) w2[M] = *(const f4*)(lds + W2F + ((M * 4 + Mp) * 64 + lane) * 4);
+#pragma unroll
+          for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int M = 0; M < 4; M++) z2[M] = mfma(w2[M][r], h1[Mp][r], z2[M]);
+        }
+#pragma unroll
+        for (int M = 0; M < 4; M++) {
+          const f4 b2 = *(const f4*)(lds + BA2 + 16 * M + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; r++) h2[M][r] = mf_lrelu(z2[M][r] + b2[r]);
+        }
+        // ---- output rows: actor z3[0..3] on h2, critic V on hc1 ----
+        float p3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, pv = 0.0f;
+#pragma unroll
+        for (int M = 0; M < 4; M++) {
+          const f4 wc2 = *(const f4*)(lds + WC2 + 16 * M + 4 * g);
+#pragma unroll
+          for (int d = 0; d < 4; d++) {
+            const f4 w3 = *(const f4*)(lds + W3 + d * 64 + 16 * M + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; r++) p3[d] = p3[d] + w3[r] * h2[M][r];
+          }
+#pragma unroll
+          for (int r = 0; r < 4; r++) pv = pv + wc2[r] * hc1[M][r];
+        }
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+          p3[d] = p3[d] + __shfl_xor(p3[d], 16);
+          p3[d] = p3[d] + __shfl_xor(p3[d], 32);
+        }
+        pv = pv + __shfl_xor(pv, 16);
+        pv = pv + __shfl_xor(pv, 32);
+        const float z3 = (g == 0 ? p3[0] : g == 1 ? p3[1] : g == 2 ? p3[2] : p3[3]) + b3g;
+        const float V = pv + bc2;
+        // ---- PPO derivative for action dimension d = g (PPOAgent.cs:234-326) ----
+        const float act = cur.act, lpo = cur.lpo, ret = cur.ret, adv = cur.adv;
+        const float mean = tanhf(z3);
+        float criticLoss = 2.0f * (V - ret);
+        float fr = (act - mean) / ga.std_;
+        fr *= fr;
+        fr /= 2.0f;
+        const float lp = ga.lp_const - fr;
+        const float rr = expf(lp - lpo);
+        const float cr = rr >= ga.upper ? ga.upper : (rr <= ga.lower ? ga.lower : rr);
+        const float cra = cr * adv, ra = rr * adv;
+        const float partA = (ra <= cra ? 1.0f : 0.0f) * adv;
+        const float partB = (cra < ra ? 1.0f : 0.0f) * adv;
+        const float partC = (rr >= ga.lower && rr <= ga.upper) ? 1.0f : 0.0f;
+        float l = partA + (partB * partC);
+        l = l * -1.0f;
+        const float eo = expf(lpo);
+        float zd = eo == 0.0f ? 1.0f : 0.0f;  // Matrix.HadamardDivision throws -> sample skipped
+        zd = fmaxf(zd, __shfl_xor(zd, 16));
+        zd = fmaxf(zd, __shfl_xor(zd, 32));
+        const bool use = valid && zd == 0.0f;
+        const float lcd = l / eo;
+        const float prob = expf(lp);
+        const float frac = (act - mean) / (ga.std_ * ga.std_);
+        float actorLoss = (prob * frac) * lcd;
+        criticLoss = use ? criticLoss / ga.b_div : 0.0f;
+        actorLoss = use ? actorLoss / ga.b_div : 0.0f;
+        const float th = mean;  // tanh(z3) again in the reference's backward pass
+        const float gz3 = actorLoss * (1.0f - (th * th));
+        float al[4], q[4];
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+          al[d] = __shfl(actorLoss, n + 16 * d);
+          q[d] = __shfl(gz3, n + 16 * d);
+        }
+        if (g == 0) {
+          diagC += criticLoss;
+          diagA += use ? ((((0.0f + al[0]) + al[1]) + al[2]) + al[3]) / 4.0f : 0.0f;
+          skipped += (valid && !use) ? 1.0f : 0.0f;
+          dbc2 += criticLoss;
+        }
+        db3 += gz3;
+        // ---- dW3 += gz3^T H2, dWc2 += dV^T Hc1 (per-lane partials over this lane's samples);
+        // gz2 = (W3^T gz3) * lrelu'(z2), gzc1 = (Wc2 dV) * lrelu'(zc1) ----
+#pragma unroll
+        for (int M = 0; M < 4; M++) {
+          const f4 wc2 = *(const f4*)(lds + WC2 + 16 * M + 4 * g);
+          f4 w3[4];
+#pragma unroll
+          for (int d = 0; d < 4; d++) w3[d] = *(const f4*)(lds + W3 + d * 64 + 16 * M + 4 * g);
+          f4 gz2, gzc1;
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+#pragma unroll
+            for (int d = 0; d < 4; d++) aw3[d][M][r] = __builtin_fmaf(q[d], h2[M][r], aw3[d][M][r]);
+            awc2[M][r] = __builtin_fmaf(criticLoss, hc1[M][r], awc2[M][r]);
+            float gh = 0.0f;
+#pragma unroll
+            for (int d = 0; d < 4; d++) gh = gh + w3[d][r] * q[d];
+            gz2[r] = gh * mf_dlrelu(h2[M][r]);
+            gzc1[r] = (0.0f + wc2[r] * criticLoss) * mf_dlrelu(hc1[M][r]);
+          }
+          db2[M] = db2[M] + gz2;
+          *(f4*)(tb + O_G2 + n * RT + 16 * M + 4 * g) = gz2;
+          *(f4*)(tb + O_GC1 + n * RT + 16 * M + 4 * g) = gzc1;
+        }
+      }
+      __syncthreads();  // chunk i's tiles to the consumer; its reads of buffer (i - 1) & 1 done
+    }
+    // ---- producer totals over the 16 sample lanes of each row ----
+#pragma unroll
+    for (int M = 0; M < 4; M++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        db2[M][r] = row_sum16(db2[M][r]);
+        awc2[M][r] = row_sum16(awc2[M][r]);
+#pragma unroll
+        for (int d = 0; d < 4; d++) aw3[d][M][r] = row_sum16(aw3[d][M][r]);
+      }
+    db3 = row_sum16(db3);
+    dbc2 = row_sum16(dbc2);
+    diagC = row_sum16(diagC);
+    diagA = row_sum16(diagA);
+    skipped = row_sum16(skipped);
+    __syncthreads();  // every wave is done with the weights and tiles
+    float* slab = lds + pair * SLAB;
+    if (lane < SLAB - (NPARAM + 3)) slab[NPARAM + 3 + lane] = 0.0f;  // (the pads)
+    if (n == 0) {
+#pragma unroll
+      for (int M = 0; M < 4; M++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int j = 16 * M + 4 * g + r;
+          slab[OFF_A_B2 + j] = db2[M][r];
+          slab[OFF_C_W2 + j] = awc2[M][r];
+#pragma unroll
+          for (int d = 0; d < 4; d++) slab[OFF_A_W3 + d * 64 + j] = aw3[d][M][r];
+        }
+      slab[OFF_A_B3 + g] = db3;
+      if (g == 0) {
+        slab[OFF_C_B2] = dbc2;
+        slab[NPARAM] = diagC;
+        slab[NPARAM + 1] = diagA;
+        slab[NPARAM + 2] = skipped;
+      }
+    }
+  } else {
+    // ---------------- consumer ----------------
+    f4 a2[4][4], a1[4], a1c[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      a1[i] = z4; a1c[i] = z4;
+#pragma unroll
+      for (int j = 0; j < 4; j++) a2[i][j] = z4;
+    }
+#pragma unroll 1
+    for (int i = 0; i <= kmax; i++) {
+#ifdef WK_WS_NOCONS  // probe: the producer alone
+      if (ga.samples < 0)
+#endif
+      if (i >= 1 && i <= kp) {
+        float* const tb = pt + ((i - 1) & 1) * TB;
+        // gz2 and h1 in N layout (the producer's own registers, read back)
+        f4 gz2[4], dh1[4];
+#pragma unroll
+        for (int M = 0; M < 4; M++) {
+          gz2[M] = *(const f4*)(tb + O_G2 + n * RT + 16 * M + 4 * g);
+          const f4 h = *(const f4*)(tb + O_H1 + n * RT + 16 * M + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; r++) dh1[M][r] = mf_dlrelu(h[r]);  // lrelu(z) < 0 iff z < 0
+        }
+        // ---- dW2 += gz2^T H1 (samples on K: step r = samples 4 g + r) ----
+        {
+          float ag[4][4], bh[4][4];
+#pragma unroll
+          for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int M = 0; M < 4; M++) {
+              ag[r][M] = tb[O_G2 + (4 * g + r) * RT + 16 * M + n];
+              bh[r][M] = tb[O_H1 + (4 * g + r) * RT + 16 * M + n];
+            }
+#pragma unroll
+          for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int Mj = 0; Mj < 4; Mj++)
+#pragma unroll
+              for (int Nk = 0; Nk < 4; Nk++) a2[Mj][Nk] = mfma(ag[r][Mj], bh[r][Nk], a2[Mj][Nk]);
+        }
+        // ---- gh1^T = W2^T gz2^T (B = gz2 registers) -> gz1 ----
+        f4 gh1[4];
+#pragma unroll
+        for (int Mk = 0; Mk < 4; Mk++) gh1[Mk] = z4;
+#pragma unroll
+        for (int Mj = 0; Mj < 4; Mj++) {
+          f4 w2[4];
+#pragma unroll
+          for (int Mk = 0; Mk < 4; Mk++) w2[Mk] = *(const f4*)(lds + W2B + ((Mk * 4 + Mj) * 64 + lane) * 4);
+#pragma unroll
+          for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int Mk = 0; Mk < 4; Mk++) gh1[Mk] = mfma(w2[Mk][r], gz2[Mj][r], gh1[Mk]);
+        }
+        wave_sync();  // the H1 reads are done: G1 goes into its buffer
+#pragma unroll
+        for (int Mk = 0; Mk < 4; Mk++) {
+          f4 gz1;
+#pragma unroll
+          for (int r = 0; r < 4; r++) gz1[r] = gh1[Mk][r] * dh1[Mk][r];
+          *(f4*)(tb + O_H1 + n * RT + 16 * Mk + 4 * g) = gz1;
+        }
+        wave_sync();
+        // ---- dW1 | db1 += gz1^T [S | 1], dWc1 | dbc1 += gzc1^T [S | 1] ----
+        {
+          float bx[4], av[4][4], acv[4][4];
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            bx[r] = tb[O_SX + (4 * g + r) * RSX + n];
+#pragma unroll
+            for (int Mj = 0; Mj < 4; Mj++) {
+              av[r][Mj] = tb[O_H1 + (4 * g + r) * RT + 16 * Mj + n];
+              acv[r][Mj] = tb[O_GC1 + (4 * g + r) * RT + 16 * Mj + n];
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int Mj = 0; Mj < 4; Mj++) {
+              a1[Mj] = mfma(av[r][Mj], bx[r], a1[Mj]);
+              a1c[Mj] = mfma(acv[r][Mj], bx[r], a1c[Mj]);
+            }
+        }
+      }
+      __syncthreads();
+    }
+    __syncthreads();  // (matches the producer's: weights and tiles are free)
+    float* slab = lds + pair * SLAB;
+#pragma unroll
+    for (int Mj = 0; Mj < 4; Mj++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int j = 16 * Mj + 4 * g + r;
+#pragma unroll
+        for (int Nk = 0; Nk < 4; Nk++) slab[OFF_A_W2 + j * 64 + 16 * Nk + n] = a2[Mj][Nk][r];
+        if (n < 12) {
+          slab[OFF_A_W1 + j * 12 + n] = a1[Mj][r];
+          slab[OFF_C_W1 + j * 12 + n] = a1c[Mj][r];
+        } else if (n == 12) {
+          slab[OFF_A_B1 + j] = a1[Mj][r];
+          slab[OFF_C_B1 + j] = a1c[Mj][r];
+        }
+      }
+  }
+  __syncthreads();
+  // the block fold over the four pair slabs, in pair order
+  f4* out = (f4*)(ga.partial + (size_t)blockIdx.x * SLAB);
+  constexpr int NV = SLAB / 4, PER = (NV + 512 - 1) / 512;
+  f4 sv[PER][PAIRS];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int i = tid + k * 512;
+#pragma unroll
+    for (int w = 0; w < PAIRS; w++) sv[k][w] = i < NV ? ((const f4*)(lds + w * SLAB))[i] : z4;
+  }
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int i = tid + k * 512;
+    f4 acc = z4;
+#pragma unroll
+    for (int w = 0; w < PAIRS; w++) acc = acc + sv[k][w];
+    if (i < NV) out[i] = acc;
+  }
+}
+
 // the weight image from the flat parameters (initialisation, wk_set_weights)
 __global__ void k_swizzle(const float* __restrict__ W, float* __restrict__ Wz) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -549,9 +999,15 @@ hipError_t launch_swizzle(const float* W, float* Wz, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifndef WK_GRAD_WS
+#define WK_GRAD_WS 1
+#endif
 hipError_t configure_mfma_kernels() {
-  return hipFuncSetAttribute((const void*)k_ppo_grad_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)(sizeof(float) * mf::LDS_FLOATS));
+  hipError_t e = hipFuncSetAttribute((const void*)k_ppo_grad_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(sizeof(float) * mf::LDS_FLOATS));
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)k_ppo_grad_ws, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)(sizeof(float) * ws::LDS_FLOATS));
 }
 
 int ppo_grad_mfma_blocks(int samples) {
@@ -561,8 +1017,11 @@ int ppo_grad_mfma_blocks(int samples) {
 }
 
 hipError_t launch_ppo_grad_mfma(const GradArgs& g, int nblocks, hipStream_t s) {
-  const size_t lds = sizeof(float) * mf::LDS_FLOATS;
-  hipLaunchKernelGGL(k_ppo_grad_mfma, dim3(nblocks), dim3(64 * mf::WAVES), lds, s, g);
+  if (WK_GRAD_WS) {
+    hipLaunchKernelGGL(k_ppo_grad_ws, dim3(nblocks), dim3(64 * 2 * ws::PAIRS), sizeof(float) * ws::LDS_FLOATS, s, g);
+  } else {
+    hipLaunchKernelGGL(k_ppo_grad_mfma, dim3(nblocks), dim3(64 * mf::WAVES), sizeof(float) * mf::LDS_FLOATS, s, g);
+  }
   return hipGetLastError();
 }
 
