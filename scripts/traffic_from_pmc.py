@@ -12,9 +12,13 @@ fetch_csv, write_csv, walkers, horizon, out = sys.argv[1:6]
 
 
 def read(path, name):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if r["Counter_Name"] == name and "k_env_s" in r["Kernel_Name"]]
-    return sum(vals) / len(vals), len(vals)
+    """mean over the rollout dispatches (the counting replay's k_env_step is not one) of the
+    counter summed over its per-unit rows"""
+    per = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == name and "k_env_side<true, true, false>" in r["Kernel_Name"]:
+            per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return sum(per.values()) / len(per), len(per)
 
 
 f_kib, nf = read(fetch_csv, "FETCH_SIZE")
