@@ -104,9 +104,11 @@ typedef struct wk_config {
   int RandomizeStart;       /* 1: env e starts at x + 200*u_e (BASELINE config 2) */
   int RandomizeMaterial;    /* 1: env material in {Ice, Rubber, Carpet} (config 5) */
   int LanesPerWalker;       /* physics kernel mapping (all bit-exact): 2 = a lane pair per
-                               walker, left / right leg chains in parallel; 16 = SAT axes
-                               over a 16-lane row; 1 = one walker per lane; 0 = auto
-                               (2 on the flat floor, 16 with RoughFloor) */
+                               walker, left / right leg chains in parallel; 4 = two lanes per
+                               leg (SAT axes and contact faces split; for shards of at most
+                               one wave per SIMD); 16 = SAT axes over a 16-lane row; 1 = one
+                               walker per lane; 0 = auto (flat floor: 4 up to 16,384
+                               walkers, else 2; 16 with RoughFloor) */
 } wk_config;
 
 /* The host-only fields of the reference's JSON configuration (SerializableHyperparameters,

@@ -238,7 +238,7 @@ static int validate(const wk_config* c, std::string& why) {
   if (c->Lambda <= 0 || c->Lambda > 1) return bad("Invalid lambda value, should be in range 0<x<1");
   if (c->Epsilon <= 0 || c->Epsilon > 1) return bad("Invalid epsilon value, should be in range 0<x<1");
   if (c->LogStandardDeviation <= -5 || c->LogStandardDeviation >= 5) return bad("Invalid log standard deviation value, should be in range -5<x<5");
-  if (c->RoughFloor && c->LanesPerWalker == 2)
+  if (c->RoughFloor && (c->LanesPerWalker == 2 || c->LanesPerWalker == 4))
     return bad("RoughFloor runs on the 1- and 16-lane mappings (LanesPerWalker 0, 1 or 16)");
   if (c->CriticNeuralNetwork && strcmp(c->CriticNeuralNetwork, kCriticDefault) != 0) {
     snprintf(b, sizeof(b), "critic network '%s' unsupported: the kernels implement '%s'", c->CriticNeuralNetwork, kCriticDefault);
@@ -253,8 +253,8 @@ static int validate(const wk_config* c, std::string& why) {
   if (c->Horizon <= 0) return bad("Horizon must be > 0");
   if (c->Minibatch < 0) return bad("Minibatch must be >= 0");
   if (c->LanesPerWalker != 0 && c->LanesPerWalker != 1 && c->LanesPerWalker != 2 &&
-      c->LanesPerWalker != 16)
-    return bad("LanesPerWalker must be 0 (auto), 1, 2 or 16");
+      c->LanesPerWalker != 4 && c->LanesPerWalker != 16)
+    return bad("LanesPerWalker must be 0 (auto), 1, 2, 4 or 16");
   return WK_OK;
 }
 
@@ -311,12 +311,14 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   P.std_ = expf(c.LogStandardDeviation);
   P.seed = seed;
   P.env_offset = c.EnvOffset;
-  // auto: the side-split pair mapping on the flat floor at every size -- measured on one
-  // MI355X (scripts/probe_small.sh, rollout T = 64): 32.1 ms at 8,192 walkers vs 83.2 ms for
-  // the 16-lane rows and 104 ms one lane per walker; 32.9 vs 62.6 / 113 ms at 4,096.  Below
-  // 32,768 walkers the pair mapping leaves SIMDs idle, but a walker's substep chain on one
-  // wave still beats its 16-fold replication.  The rough floor runs on the 16-lane rows.
-  P.lanes = c.LanesPerWalker ? c.LanesPerWalker : (c.RoughFloor ? 16 : 2);
+  // auto on the flat floor: the side-split pair mapping from 16,385 walkers up, the quad
+  // mapping (two lanes per leg) below -- measured on one MI355X (scripts/side_times.sh,
+  // rollout T = 16): 5.94 vs 7.56 ms at 8,192 and 16,384 walkers (one wave per SIMD at most,
+  // where the split shortens each wave's chain), 11.7 vs 7.6 ms at 32,768 (two waves per
+  // SIMD: issue-bound, the split's extra selects and exchanges cost more than they save).
+  // Round 1: the pair mapping 32.1 ms at 8,192 walkers vs 83.2 ms for the 16-lane rows and
+  // 104 ms one lane per walker (T = 64).  The rough floor runs on the 16-lane rows.
+  P.lanes = c.LanesPerWalker ? c.LanesPerWalker : (c.RoughFloor ? 16 : (n_env <= 16384 ? 4 : 2));
   P.rough = c.RoughFloor ? 1 : 0;
   const float PI_F = 3.14159265358979323846f;
   x->lp_const = -logf(P.std_) - logf(sqrtf(2.0f * PI_F));

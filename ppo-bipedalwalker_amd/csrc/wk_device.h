@@ -291,11 +291,12 @@ DEV void proj_minmax(const Poly<N>& P, float ax, float ay, float& mn, float& mx)
 //
 // AX (optional): the normalised axes, kept for the contact faces (see EdgeAxes).
 template <int N> struct EdgeAxes { float x[N], y[N]; };
-template <int NP, int NQ, bool FLOORQ = false, bool ZE = false>
+// NE: only P's first NE edges (the quad mapping's halves of an axis list).
+template <int NP, int NQ, bool FLOORQ = false, bool ZE = false, int NE = NP>
 DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, float& depth,
                    EdgeAxes<NP>* AX = nullptr) {
 #pragma unroll
-  for (int i = 0; i < NP; i++) {
+  for (int i = 0; i < NE; i++) {
     const int i1 = (i + 1) % NP;
     const float ex = P.x[i1] - P.x[i], ey = P.y[i1] - P.y[i];
     V2 axis = mk(-ey, ex);
@@ -582,14 +583,11 @@ DEV int clip_vectors(V2 a, V2 b, V2 n, float offset, V2& o0, V2& o1) {
   return (int)ka + (int)kb + (int)kx;
 }
 
-// GetContactPoints with both polygons' SAT axes kept: the faces' directions come normalised
-template <int NA, int NB>
-DEV int contact_points_ax(const Poly<NA>& A, const EdgeAxes<NA>& AXA, const Poly<NB>& B,
-                          const EdgeAxes<NB>& AXB, V2 normal, V2& c0, V2& c1) {
-  V2 ra, rb, rmax, rd, ia, ib, imax, id;
-  significant_face_ax(A, AXA, normal, ra, rb, rmax, rd);
+// GetContactPoints (:13-53) from the two significant faces (A's on the normal, B's on its
+// negation: vertices a, b, the max vertex and the normalised face direction)
+DEV int contact_clip(V2 ra, V2 rb, V2 rmax, V2 rd, V2 ia, V2 ib, V2 imax, V2 id, V2 normal,
+                     V2& c0, V2& c1) {
   V2 rf = vsub(rb, ra);
-  significant_face_ax(B, AXB, vneg(normal), ia, ib, imax, id);
   V2 iv = vsub(ib, ia);
   if (fabsf(vdot(rf, normal)) > fabsf(vdot(iv, normal))) {  // selects, not a branch
     V2 t;
@@ -615,6 +613,15 @@ DEV int contact_points_ax(const Poly<NA>& A, const EdgeAxes<NA>& AXA, const Poly
   c0 = q0;
   c1 = q1;
   return cnt;
+}
+// GetContactPoints with both polygons' SAT axes kept: the faces' directions come normalised
+template <int NA, int NB>
+DEV int contact_points_ax(const Poly<NA>& A, const EdgeAxes<NA>& AXA, const Poly<NB>& B,
+                          const EdgeAxes<NB>& AXB, V2 normal, V2& c0, V2& c1) {
+  V2 ra, rb, rmax, rd, ia, ib, imax, id;
+  significant_face_ax(A, AXA, normal, ra, rb, rmax, rd);
+  significant_face_ax(B, AXB, vneg(normal), ia, ib, imax, id);
+  return contact_clip(ra, rb, rmax, rd, ia, ib, imax, id, normal, c0, c1);
 }
 
 template <int NA, int NB, bool SAFE = false>

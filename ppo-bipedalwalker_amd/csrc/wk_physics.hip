@@ -206,14 +206,120 @@ DEV Poly<N> perturbed(const Poly<N>& p) {
 #define DUP(k, ...) do {} while (0)
 #endif
 
+// ---------------- quad mapping helpers (L = 4: two lanes per leg) ----------------
+// The lane pair of a leg (halves 0 and 1: quad_perm [2,3,0,1] partners) holds the same leg
+// state and splits the heavy halves of its pairs; each half ends with the other's results
+// (DPP) combined in the reference's order, so both hold identical values throughout.
+DEV float hswap(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+// per-lane selects as bit masks: a ?: between register copies can be folded by LLVM into a
+// load through a selected address, which moves the polygons to scratch memory (cf. pick)
+DEV float fsel(uint32_t m, float a, float b) { return __uint_as_float(bsel(m, a, __float_as_uint(b))); }
+template <int N>
+DEV Poly<N> psel(bool c, const Poly<N>& a, const Poly<N>& b) {
+  const uint32_t m = c ? 0xffffffffu : 0u;
+  Poly<N> r;
+#pragma unroll
+  for (int i = 0; i < N; i++) { r.x[i] = fsel(m, a.x[i], b.x[i]); r.y[i] = fsel(m, a.y[i], b.y[i]); }
+  r.cx = fsel(m, a.cx, b.cx);
+  r.cy = fsel(m, a.cy, b.cy);
+  return r;
+}
+// AxisChecks(A's edges, B) on half 0 and AxisChecks(B's edges, A) on half 1, then
+// SATCollision's order: A's axes first, B's best only when strictly smaller (axis_pass
+// takes on temp < depth, so the sequential result is the first strict minimum over A's axes
+// then B's).  P / AXP: this half's own polygon and its normalised axes (for its face).
+template <int N>
+DEV bool sat_split(const Poly<N>& A, const Poly<N>& B, int half, V2& normal, float& depth,
+                   Poly<N>& P, EdgeAxes<N>& AXP) {
+  P = psel(half != 0, B, A);
+  const Poly<N> Q = psel(half != 0, A, B);
+  bool sep = false;
+  V2 nn = mk(0.0f, 0.0f);
+  float dd = FLT_MAX;
+  axis_pass<N, N, false, false>(P, Q, sep, nn, dd, &AXP);
+  const bool sep_o = hswap(sep ? 1.0f : 0.0f) != 0.0f;
+  const float dd_o = hswap(dd), nx_o = hswap(nn.x), ny_o = hswap(nn.y);
+  const float dA = half ? dd_o : dd, dB = half ? dd : dd_o;
+  const V2 nA = half ? mk(nx_o, ny_o) : nn, nB = half ? nn : mk(nx_o, ny_o);
+  const bool takeB = dB < dA;
+  depth = takeB ? dB : dA;
+  normal = takeB ? nB : nA;
+  const V2 dir = mk(B.cx - A.cx, B.cy - A.cy);
+  if (vdot(dir, normal) > 0.0f) normal = vmul(normal, -1.0f);
+  return !(sep || sep_o);
+}
+// GetContactPoints with the two faces split: half 0 A's on the normal, half 1 B's on its
+// negation (each from its own SAT axes), exchanged, then the clipping in both
+template <int N>
+DEV int contacts_split(const Poly<N>& P, const EdgeAxes<N>& AXP, int half, V2 normal, V2& c0,
+                       V2& c1) {
+  V2 fa, fb, fm, fd;
+  significant_face_ax(P, AXP, half ? vneg(normal) : normal, fa, fb, fm, fd);
+  const V2 oa = mk(hswap(fa.x), hswap(fa.y)), ob = mk(hswap(fb.x), hswap(fb.y));
+  const V2 om = mk(hswap(fm.x), hswap(fm.y)), od = mk(hswap(fd.x), hswap(fd.y));
+  const bool h = half != 0;
+  return contact_clip(h ? oa : fa, h ? ob : fb, h ? om : fm, h ? od : fd,
+                      h ? fa : oa, h ? fb : ob, h ? fm : om, h ? fd : od, normal, c0, c1);
+}
+// SAT of a leg segment against the flat floor with the segment's six axes split three and
+// three (half 1 walks the segment from vertex 3: its edges 0..2 are edges 3..5, the same
+// vertex set projected), then the floor's four closed-form axes in both; every axis of A
+// ends up in AX on both halves (for A's contact face)
+DEV bool sat_floor_split(const Poly<6>& A, const Poly<4>& F, float mnx, float mny, float mxx,
+                         float mxy, int half, V2& normal, float& depth, EdgeAxes<6>& AX) {
+  Poly<6> R;
+  const uint32_t hm = half ? 0xffffffffu : 0u;
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    R.x[i] = fsel(hm, A.x[(i + 3) % 6], A.x[i]);
+    R.y[i] = fsel(hm, A.y[(i + 3) % 6], A.y[i]);
+  }
+  R.cx = A.cx;
+  R.cy = A.cy;
+  bool sep = false;
+  V2 nn = mk(0.0f, 0.0f);
+  float dd = FLT_MAX;
+  EdgeAxes<6> own;
+  axis_pass<6, 4, true, false, 3>(R, F, sep, nn, dd, &own);
+  const bool sep_o = hswap(sep ? 1.0f : 0.0f) != 0.0f;
+  const float dd_o = hswap(dd), nx_o = hswap(nn.x), ny_o = hswap(nn.y);
+  const float d0 = half ? dd_o : dd, d1 = half ? dd : dd_o;
+  const V2 n0 = half ? mk(nx_o, ny_o) : nn, n1 = half ? nn : mk(nx_o, ny_o);
+  const bool take1 = d1 < d0;
+  depth = take1 ? d1 : d0;
+  normal = take1 ? n1 : n0;
+  sep = sep || sep_o;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const float ox = hswap(own.x[i]), oy = hswap(own.y[i]);
+    AX.x[i] = half ? ox : own.x[i];
+    AX.y[i] = half ? oy : own.y[i];
+    AX.x[i + 3] = half ? own.x[i] : ox;
+    AX.y[i + 3] = half ? own.y[i] : oy;
+  }
+  floor_axis(-50.0f, 1050.0f, mnx, mxx, 1.0f, 0.0f, sep, normal, depth);
+  floor_axis(900.0f, 1050.0f, mny, mxy, -0.0f, 1.0f, sep, normal, depth);
+  floor_axis(-1050.0f, 50.0f, -mxx, -mnx, -1.0f, 0.0f, sep, normal, depth);
+  floor_axis(-1050.0f, -900.0f, -mxy, -mny, -0.0f, -1.0f, sep, normal, depth);
+  V2 dir = mk(F.cx - A.cx, F.cy - A.cy);
+  if (vdot(dir, normal) > 0.0f) normal = vmul(normal, -1.0f);
+  return !sep;
+}
+
 // RigidBody.ResolveCollisions body for one (this=A, other=B) candidate
 // (Bodies/RigidBody.cs:66-96); B may be the static floor.  GENERIC: B is a static floor
 // polygon other than the flat box (a rough-floor segment): its bounding box, SAT and
 // contact faces are evaluated in general, with Vector2.Normalize's NaN for a zero edge.
-template <int NA, int NB, bool BSTATIC, bool TRACE, int L, bool GENERIC = false>
+// H = 2: the quad mapping (sub = this lane's half): SAT axes and contact faces split over
+// the leg's two lanes (leg-leg and leg-floor pairs of Poly<6> segments).
+template <int NA, int NB, bool BSTATIC, bool TRACE, int L, bool GENERIC = false, int H = 1>
 DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB,
                       bool& colA, PairTraceDev* tr, int pi, int sub, RegionProf* rp = nullptr,
                       uint32_t* ec = nullptr) {
+  static_assert(H == 1 || (L == 1 && !GENERIC && NA == 6 && NB == (BSTATIC ? 4 : 6)),
+                "the quad split covers leg-leg and leg-floor pairs");
   static_assert(!BSTATIC || NB == 4, "the static body is the floor");
   static_assert(!GENERIC || BSTATIC, "generic static floor polygon");
   constexpr bool FLAT = BSTATIC && !GENERIC;
@@ -241,7 +347,10 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   constexpr bool KEEP = L == 1 && !GENERIC;
   EdgeAxes<NA> axa;
   EdgeAxes<NB> axb;
-  if constexpr (L > 1) hit = sat_row<L>(A, B, sub, n, depth);
+  Poly<NA> own;  // H = 2 leg-leg: this half's polygon (A or B) and its axes (in axa)
+  if constexpr (H == 2 && FLAT) hit = sat_floor_split(A, B, mnx, mny, mxx, mxy, sub, n, depth, axa);
+  else if constexpr (H == 2) hit = sat_split(A, B, sub, n, depth, own, axa);
+  else if constexpr (L > 1) hit = sat_row<L>(A, B, sub, n, depth);
   else if constexpr (FLAT) hit = sat_floor(A, B, mnx, mny, mxx, mxy, n, depth, &axa);
   else if constexpr (KEEP) hit = sat<NA, NB, false>(A, B, n, depth, &axa, &axb);
   else hit = sat<NA, NB, GENERIC>(A, B, n, depth);
@@ -252,7 +361,8 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   if (ec) ec[EV_SAT_LL + EVK]++;
   V2 c0, c1;
   int nc;
-  if constexpr (KEEP && FLAT) nc = contact_points_ax(A, axa, B, floor_axes(), n, c0, c1);
+  if constexpr (H == 2 && !BSTATIC) nc = contacts_split(own, axa, sub, n, c0, c1);
+  else if constexpr (KEEP && FLAT) nc = contact_points_ax(A, axa, B, floor_axes(), n, c0, c1);
   else if constexpr (KEEP) nc = contact_points_ax(A, axa, B, axb, n, c0, c1);
   else nc = contact_points<NA, NB, GENERIC>(A, B, n, c0, c1);
   rp_mark(rp, RP_CONTACT);
@@ -831,9 +941,9 @@ DEV void get_obs_side(const SideState& s, int side, float o[12]) {
   o[11] = left ? otup : tup;
 }
 
-template <bool TRACE>
+template <bool TRACE, int Q>
 DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
-                      PairTraceDev* tr, int side, RegionProf* rp) {
+                      PairTraceDev* tr, int side, int half, RegionProf* rp) {
   rp_mark(rp, RP_OTHER);
   Poly<4> fl;
   floor_poly(fl);
@@ -860,16 +970,16 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
            sink(l2.x[0]); sink(l2.y[5]); sink(d2.th); });
 #pragma unroll
   for (int q = 0; q < 3; q++) {  // [floor if post], other segment, [floor if episode 0]
-    if (q == 1) resolve_pair<6, 6, false, TRACE, 1>(s.lo, s.dlo, mp, s.up, s.dup, mp, s.clo, tr, pb + 0, 0, rp);
-    else if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1>(s.lo, s.dlo, mp, fl, dfl, mf, s.clo, tr, pb + 1, 0, rp);
+    if (q == 1) resolve_pair<6, 6, false, TRACE, 1, false, Q>(s.lo, s.dlo, mp, s.up, s.dup, mp, s.clo, tr, pb + 0, half, rp);
+    else if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1, false, Q>(s.lo, s.dlo, mp, fl, dfl, mf, s.clo, tr, pb + 1, half, rp);
     rp_mark(rp, RP_OTHER);
   }
   integrate(s.up, s.dup, dt, adx, ady);
   rp_mark(rp, RP_INTEG);
 #pragma unroll
   for (int q = 0; q < 3; q++) {
-    if (q == 1) resolve_pair<6, 6, false, TRACE, 1>(s.up, s.dup, mp, s.lo, s.dlo, mp, s.cup, tr, pb + 2, 0, rp);
-    else if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1>(s.up, s.dup, mp, fl, dfl, mf, s.cup, tr, pb + 3, 0, rp);
+    if (q == 1) resolve_pair<6, 6, false, TRACE, 1, false, Q>(s.up, s.dup, mp, s.lo, s.dlo, mp, s.cup, tr, pb + 2, half, rp);
+    else if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1, false, Q>(s.up, s.dup, mp, fl, dfl, mf, s.cup, tr, pb + 3, half, rp);
     rp_mark(rp, RP_OTHER);
   }
   // the torso's step, replicated in both lanes (traced by the left lane)
@@ -904,13 +1014,16 @@ DEV void st_nt4(float* p, float a, float b, float c, float d) {
 DEV pf4 pmfma(float a, float b, pf4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 DEV float plrelu(float z) { return z < 0.0f ? 0.2f * z : z; }  // == Math.Max(0.2 z, z), see mf_lrelu
 
-DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], int side,
+// Q = 2 (quad mapping): 16 walkers per wave, one N tile
+template <int Q>
+DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool writer,
                      float* __restrict__ pl, float z3[4], float& value) {
   using namespace mf;
-  const int lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4, wl = lane >> 1;
+  constexpr int NT = 2 / Q;  // 16-walker tiles per wave
+  const int lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4, wl = lane >> (Q == 2 ? 2 : 1);
   float* tile = pl;          // [32 walkers][16]: 12 observations
   float* outs = pl + 512;    // [32 walkers][8]: z3[0..3], critic output
-  if (side == 0) {
+  if (writer) {
 #pragma unroll
     for (int q = 0; q < 3; q++) {
       const pf4 v = {obs[4 * q], obs[4 * q + 1], obs[4 * q + 2], obs[4 * q + 3]};
@@ -918,14 +1031,16 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], int side
     }
   }
   wave_lds_sync();
-  float sB[2][3];
+  float sB[NT][3];
 #pragma unroll
-  for (int nt = 0; nt < 2; nt++)
+  for (int nt = 0; nt < NT; nt++)
 #pragma unroll
     for (int t = 0; t < 3; t++) sB[nt][t] = tile[(16 * nt + n) * 16 + 4 * t + g];
   const pf4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
-  pf4 h1[2][4];
-  float pv[2] = {0.0f, 0.0f};
+  pf4 h1[NT][4];
+  float pv[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; nt++) pv[nt] = 0.0f;
 #pragma unroll
   for (int Mt = 0; Mt < 4; Mt++) {
     float wa[3], wc[3];
@@ -938,7 +1053,7 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], int side
     const pf4 bc = *(const pf4*)(Wz + BC1 + 16 * Mt + 4 * g);
     const pf4 w2c = *(const pf4*)(Wz + WC2 + 16 * Mt + 4 * g);
 #pragma unroll
-    for (int nt = 0; nt < 2; nt++) {
+    for (int nt = 0; nt < NT; nt++) {
       pf4 acc = z4, accc = z4;
 #pragma unroll
       for (int t = 0; t < 3; t++) {
@@ -952,28 +1067,30 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], int side
       }
     }
   }
-  float p3[2][4];
+  float p3[NT][4];
 #pragma unroll
-  for (int nt = 0; nt < 2; nt++)
+  for (int nt = 0; nt < NT; nt++)
 #pragma unroll
     for (int d = 0; d < 4; d++) p3[nt][d] = 0.0f;
 #pragma unroll 1
   for (int Mt = 0; Mt < 4; Mt++) {  // not unrolled: keeps one Mt's weights in flight
-    pf4 acc[2] = {z4, z4};
+    pf4 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; nt++) acc[nt] = z4;
 #pragma unroll
     for (int Mp = 0; Mp < 4; Mp++) {
       const pf4 w = *(const pf4*)(Wz + W2F + ((Mt * 4 + Mp) * 64 + lane) * 4);
 #pragma unroll
       for (int r = 0; r < 4; r++)
 #pragma unroll
-        for (int nt = 0; nt < 2; nt++) acc[nt] = pmfma(w[r], h1[nt][Mp][r], acc[nt]);
+        for (int nt = 0; nt < NT; nt++) acc[nt] = pmfma(w[r], h1[nt][Mp][r], acc[nt]);
     }
     const pf4 b2 = *(const pf4*)(Wz + BA2 + 16 * Mt + 4 * g);
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int k = 16 * Mt + 4 * g + r;
 #pragma unroll
-      for (int nt = 0; nt < 2; nt++) {
+      for (int nt = 0; nt < NT; nt++) {
         const float h2 = plrelu(acc[nt][r] + b2[r]);
 #pragma unroll
         for (int d = 0; d < 4; d++) p3[nt][d] = p3[nt][d] + Wz[W3 + d * 64 + k] * h2;
@@ -981,7 +1098,7 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], int side
     }
   }
 #pragma unroll
-  for (int nt = 0; nt < 2; nt++) {
+  for (int nt = 0; nt < NT; nt++) {
 #pragma unroll
     for (int d = 0; d < 4; d++) {
       p3[nt][d] = p3[nt][d] + __shfl_xor(p3[nt][d], 16);
@@ -993,7 +1110,7 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], int side
   wave_lds_sync();  // the tile reads above are done before the outputs reuse LDS
   if (g == 0) {
 #pragma unroll
-    for (int nt = 0; nt < 2; nt++) {
+    for (int nt = 0; nt < NT; nt++) {
       const pf4 v = {p3[nt][0], p3[nt][1], p3[nt][2], p3[nt][3]};
       *(pf4*)(outs + (16 * nt + n) * 8) = v;
       outs[(16 * nt + n) * 8 + 4] = pv[nt];
@@ -1008,17 +1125,27 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], int side
   wave_lds_sync();  // outputs read before the next env-step rewrites the tile
 }
 
-constexpr int SIDE_BLOCK = 256;  // 4 waves: the policy's weight image is staged once per block
-template <bool POLICY, bool RECORD, bool TRACE>
-__global__ __launch_bounds__(SIDE_BLOCK) WK_ENV_WPE void k_env_side(EnvParams P, StepArgs A) {
+#ifndef WK_SIDE_BLOCK
+#define WK_SIDE_BLOCK 256
+#endif
+constexpr int SIDE_BLOCK = WK_SIDE_BLOCK;  // 4 waves: the policy's weight image is staged once per block
+// Q = 1: a lane pair per walker (L = 2); Q = 2: a lane quad (L = 4, side = lane bit 0, half =
+// lane bit 1), for shards of at most one wave per SIMD, where the split shortens each wave's
+// dependent chain -- with room for every register (one wave per SIMD: no spills)
+template <bool POLICY, bool RECORD, bool TRACE, int Q>
+__global__ __launch_bounds__(SIDE_BLOCK)
+__attribute__((amdgpu_waves_per_eu(Q == 2 ? 1 : WK_ENV_WAVES, Q == 2 ? 1 : WK_ENV_WAVES)))
+void k_env_side(EnvParams P, StepArgs A) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int side = tid & 1;
+  const int half = Q == 2 ? (tid >> 1) & 1 : 0;
+  constexpr int SH = Q == 2 ? 2 : 1;  // log2 lanes per walker
   const int n = P.n_env;
   // a partial last wave keeps every lane (the policy's MFMAs need the whole wave):
-  // out-of-range pairs replay walker n-1 and never store
-  const bool active = (tid >> 1) < n;
-  const int e = active ? (tid >> 1) : n - 1;
-  const bool leader = side == 0 && active;
+  // out-of-range lanes replay walker n-1 and never store
+  const bool active = (tid >> SH) < n;
+  const int e = active ? (tid >> SH) : n - 1;
+  const bool leader = side == 0 && half == 0 && active;
   __shared__ float pol_lds[POLICY ? (SIDE_BLOCK / 64) * 768 : 1];
   __shared__ float wz_lds[POLICY ? mf::WEND : 1];  // operand-order weights (41 KB, 2 blocks/CU)
   if (POLICY) {
@@ -1053,7 +1180,7 @@ __global__ __launch_bounds__(SIDE_BLOCK) WK_ENV_WPE void k_env_side(EnvParams P,
     if (POLICY) {
       get_obs_side(s, side, obs);
       float z3[4], mean[4], v;
-      policy_mfma(wz_lds, obs, side, wave_pol, z3, v);
+      policy_mfma<Q>(wz_lds, obs, side == 0 && half == 0, wave_pol, z3, v);
 #pragma unroll
       for (int d = 0; d < 4; d++) mean[d] = tanhf(z3[d]);
       sample_actions(P, A.lp_const, gid, t, mean, a, lp);
@@ -1080,8 +1207,8 @@ __global__ __launch_bounds__(SIDE_BLOCK) WK_ENV_WPE void k_env_side(EnvParams P,
     }
 #pragma unroll 1
     for (int it = 0; it < P.iterations; it++) {
-      PairTraceDev* tr = (TRACE && active) ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
-      substep_side<TRACE>(s, mp, mb, dt, adx, ady, tr, side, rp);
+      PairTraceDev* tr = (TRACE && active && half == 0) ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
+      substep_side<TRACE, Q>(s, mp, mb, dt, adx, ady, tr, side, half, rp);
     }
     // Walker.Update + terminal flags (both upper legs and the torso)
     s.prevx = s.posx; s.prevy = s.posy;
@@ -1127,7 +1254,7 @@ __global__ __launch_bounds__(SIDE_BLOCK) WK_ENV_WPE void k_env_side(EnvParams P,
     }
     t++;
   }
-  if (active) store_side(s, A.st, e, side);
+  if (active && half == 0) store_side(s, A.st, e, side);
 #ifdef WK_REGION_PROF
   if ((threadIdx.x & 63) == 0)
     for (int r = 0; r < 8; r++) atomicAdd(&g_region_prof[r], (unsigned long long)rpv.acc[r]);
@@ -1241,13 +1368,14 @@ static void launch_lanes(int mode, const EnvParams& P, const StepArgs& A, hipStr
   if (P.rough) launch_lanes_floor<L, true>(mode, P, A, s);
   else launch_lanes_floor<L, false>(mode, P, A, s);
 }
+template <int Q>
 static void launch_side(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
-  dim3 blk(SIDE_BLOCK), grd((unsigned)(((size_t)P.n_env * 2 + SIDE_BLOCK - 1) / SIDE_BLOCK));
+  dim3 blk(SIDE_BLOCK), grd((unsigned)(((size_t)P.n_env * 2 * Q + SIDE_BLOCK - 1) / SIDE_BLOCK));
   switch (mode) {
-    case 0: hipLaunchKernelGGL((k_env_side<false, false, false>), grd, blk, 0, s, P, A); break;
-    case 1: hipLaunchKernelGGL((k_env_side<false, false, true>), grd, blk, 0, s, P, A); break;
-    case 2: hipLaunchKernelGGL((k_env_side<true, false, false>), grd, blk, 0, s, P, A); break;
-    default: hipLaunchKernelGGL((k_env_side<true, true, false>), grd, blk, 0, s, P, A); break;
+    case 0: hipLaunchKernelGGL((k_env_side<false, false, false, Q>), grd, blk, 0, s, P, A); break;
+    case 1: hipLaunchKernelGGL((k_env_side<false, false, true, Q>), grd, blk, 0, s, P, A); break;
+    case 2: hipLaunchKernelGGL((k_env_side<true, false, false, Q>), grd, blk, 0, s, P, A); break;
+    default: hipLaunchKernelGGL((k_env_side<true, true, false, Q>), grd, blk, 0, s, P, A); break;
   }
 }
 hipError_t launch_env_scene(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
@@ -1268,7 +1396,8 @@ hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipS
     hipLaunchKernelGGL((k_env_step<false, false, false, 1, false, true>), grd, blk, 0, s, P, A);
     return hipGetLastError();
   }
-  if (P.lanes == 2) launch_side(mode, P, A, s);
+  if (P.lanes == 2) launch_side<1>(mode, P, A, s);
+  else if (P.lanes == 4) launch_side<2>(mode, P, A, s);
   else if (P.lanes == 16) launch_lanes<16>(mode, P, A, s);
   else launch_lanes<1>(mode, P, A, s);
   return hipGetLastError();

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 
 SEED = 20250905
 F = np.float32
-LANES = [1, 2, 16]  # physics mappings: lane per walker, side-split pair, SAT rows
+LANES = [1, 2, 4, 16]  # physics mappings: lane per walker, side-split pair, split leg pairs, SAT rows
 lanes_param = pytest.mark.parametrize("lanes", LANES)
 
 
