@@ -35,7 +35,7 @@ public struct WkConfig
     public IntPtr CriticNeuralNetwork, ActorNeuralNetwork;  // NULL = the default networks
     public float DeltaTime;
     public int Horizon, Minibatch, MinibatchGlobal, EnvOffset, RandomizeStart, RandomizeMaterial;
-    public int LanesPerWalker;  // 0 = auto (2-lane leg split; 16-lane rows with RoughFloor)
+    public int LanesPerWalker;  // 0 = auto (4-lane split leg pairs up to 16,384 walkers, else the 2-lane leg split; 16-lane rows with RoughFloor)
 }
 
 // SerializableHyperparameters' host-only fields (Hyperparameters.cs:11-77)
