@@ -599,7 +599,11 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
   }
   pair = __builtin_amdgcn_readfirstlane(pair);
   producer = __builtin_amdgcn_readfirstlane(producer ? 1 : 0) != 0;
+#ifdef WK_GRAD_NOLOOP  // probe: the launch without its chunk loop (fixed-cost measurement)
+  const int nchunks = 0;
+#else
   const int nchunks = (ga.samples + 15) / 16;
+#endif
   const int nw = gridDim.x * PAIRS;
   const int c0 = blockIdx.x * PAIRS + pair;
   const int kp = c0 < nchunks ? (nchunks - 1 - c0) / nw + 1 : 0;         // this pair's chunks
@@ -621,6 +625,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
   };
   Smp nxt;
   if (producer) nxt = gather(c0 < nchunks ? c0 : 0);  // in flight while the weights are staged
+#ifndef WK_GRAD_NOSTAGE  // probe: no weight staging (fixed-cost measurement)
   {
     constexpr int NV = WEND / 4, PER = (NV + 512 - 1) / 512;
     f4 wv[PER];
@@ -635,6 +640,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
       if (e < NV) ((f4*)lds)[e] = wv[i];
     }
   }
+#endif
   __syncthreads();
   float* const pt = lds + WEND + pair * 2 * TB;  // this pair's two tile buffers
   const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -813,6 +819,9 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
       }
       __syncthreads();  // chunk i's tiles to the consumer; its reads of buffer (i - 1) & 1 done
     }
+#ifdef WK_GRAD_NOEPI  // probe: no epilogue
+    if (ga.samples >= 0) return;
+#endif
     // ---- producer totals over the 16 sample lanes of each row ----
 #pragma unroll
     for (int M = 0; M < 4; M++)
@@ -938,6 +947,9 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
       }
       __syncthreads();
     }
+#ifdef WK_GRAD_NOEPI
+    if (ga.samples >= 0) return;
+#endif
     __syncthreads();  // (matches the producer's: weights and tiles are free)
     float* slab = lds + pair * SLAB;
 #pragma unroll

@@ -6,7 +6,8 @@ import wk
 n, T = 65536, 64
 eng = wk.Engine(n, seed=20250905, Horizon=T, RandomizeStart=1, Minibatch=n, Epochs=1)
 eng.rollout(T)
-for M in (16384, 32768, 65536, 131072, 262144):
+sizes = [int(x) for x in os.environ.get("WK_GRAD_SIZES", "16384 32768 65536 131072 262144").split()]
+for M in sizes:
     eng.ppo_update(minibatch=M, update_index=0)
     eng.sync()
     eng.profile_reset(); eng.profile_enable(2)
