@@ -79,6 +79,10 @@ def parse():
                    help="skip the configs 2 / 3 / 4-shard / 5-shard lines (N = 1 only)")
     p.add_argument("--cpu-baseline-steps", type=int, default=150000)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--rehearse", action="store_true",
+                   help="multi-rank rehearsal on ONE GPU: every rank on device 0, gradients "
+                        "all-reduced on the host over gloo (wk_comm_init_host) instead of RCCL "
+                        "-- exercises the N > 1 code path; not a performance number")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_physics.json"))
     return p.parse_args()
 
@@ -248,6 +252,8 @@ def main():
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group("gloo")  # control plane only; gradients go over RCCL
+    if args.rehearse:
+        local = 0
     torch.cuda.set_device(local)
     weak = args.walkers > 0
     if weak:
@@ -266,7 +272,12 @@ def main():
                     Minibatch=shard.minibatch_local, MinibatchGlobal=shard.minibatch_global,
                     Epochs=args.epochs, EnvOffset=shard.env_offset, RandomizeStart=1,
                     RandomizeMaterial=1 if args.materials else 0, LanesPerWalker=args.lanes)
-    if world > 1:
+    if world > 1 and args.rehearse:
+        def host_allreduce(buf):
+            t = torch.from_numpy(buf)
+            dist.all_reduce(t)  # in place on the numpy view (gloo)
+        eng.comm_init_host(rank, world, host_allreduce)
+    elif world > 1:
         uid = wk.Engine.comm_unique_id() if rank == 0 else None
         uid = broadcast_unique_id(uid)
         eng.comm_init(rank, world, uid)
@@ -321,8 +332,10 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
-    lanes = args.lanes or 2
-    kernel = {2: "k_env_side<true,true,false>", 16: "k_env_step<true,true,false,16,false>",
+    # the mapping wk_create picks (include/wk_api.h, LanesPerWalker 0 = auto)
+    lanes = args.lanes or (4 if shard.n_local <= 16384 else 2)
+    kernel = {2: "k_env_side<true,true,false,1>", 4: "k_env_side<true,true,false,2> (quad mapping)",
+              16: "k_env_step<true,true,false,16,false>",
               1: "k_env_step<true,true,false,1,false>"}[lanes]
     alg_bytes = alg_bytes_per_env_step(T) * units
     out = {
@@ -393,6 +406,9 @@ def main():
         out["configs"] = ex
     if cpu is not None:
         out["cpu_baseline"] = cpu
+    if args.rehearse:
+        out["rehearsal"] = ("all ranks on one GPU, host all-reduce over gloo: a check of the "
+                            "multi-rank path, not a performance number")
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

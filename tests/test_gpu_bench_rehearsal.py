@@ -1,0 +1,42 @@
+"""GPU: bench.py's multi-rank path end to end on one GPU (`--rehearse`): two ranks launched as
+the driver launches the 8-GPU run (torch.distributed.run, 127.0.0.1), both on device 0, the
+per-minibatch all-reduce on the host over gloo (RCCL refuses two ranks on one device).  Checks
+the launcher plumbing, the strong-scaling shard (walkers and minibatch split over the ranks),
+the barrier / max-over-ranks timing and the one JSON line from rank 0 -- not a performance
+number.  Small shapes: 4,096 global walkers (2,048 per rank: the quad mapping), T = 8."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_rank_rehearsal():
+    cmd = ["timeout", "-k", "10", "240", sys.executable, "-m", "torch.distributed.run",
+           "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--rehearse", "--walkers-global", "4096",
+           "--horizon", "8", "--epochs", "1", "--regime-iters", "1"]
+    p = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    assert p.returncode == 0, p.stdout[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-3000:]  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong" and "rehearsal" in out
+    assert out["config"]["walkers_per_gpu"] == 2048 and out["config"]["global_walkers"] == 4096
+    assert out["config"]["minibatch_global"] == 4096
+    assert "quad" in out["roofline"]["kernel"]
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    assert abs(out["value"] - 4096 * 8 * 2 / (out["ms_per_step"] * 2e-3)) < 1e-6 * out["value"]
