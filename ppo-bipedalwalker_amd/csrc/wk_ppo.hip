@@ -325,31 +325,40 @@ __global__ void k_grad_reduce2_adam(const float* __restrict__ part2, int ngroups
 }
 
 // One-launch form of the two stages for nblocks <= RG * RG, bit-identical association
-// (RG consecutive slabs in order, then the groups in order): a block owns 16 parameters;
-// thread (group gi, parameter pi) folds its group's RG slabs, and the 16 group sums are
-// folded in order through LDS.  ADAM: the single-GPU tail applies Adam as well.
+// (RG consecutive slabs in order, then the groups in order): a block owns 16 parameter
+// quads; thread (group gi, quad qi) folds its group's RG slabs with 16-byte loads (all issued
+// before the ordered adds), and the 16 group sums are folded in order through LDS.  ADAM: the
+// single-GPU tail applies Adam as well.
 template <bool ADAM>
 __global__ __launch_bounds__(256) void k_grad_reduce_fused(const float* __restrict__ partial,
                                                            int nblocks, float* grad, AdamArgs a) {
-  __shared__ float gs[RG][17];
-  const int pi = threadIdx.x & 15, gi = threadIdx.x >> 4;
-  const int p = blockIdx.x * 16 + pi;
+  static_assert(SLAB % 4 == 0, "16-byte slab rows");
+  __shared__ float4 gs[RG][16];
+  const int qi = threadIdx.x & 15, gi = threadIdx.x >> 4;
+  const int q = blockIdx.x * 16 + qi;  // parameters 4q .. 4q + 3
   const int ngroups = (nblocks + RG - 1) / RG;
-  float acc = 0.0f;
-  if (p < SLAB && gi < ngroups) {
+  float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (q < SLAB / 4 && gi < ngroups) {
     const int b0 = gi * RG;
-    float v[RG];
-#pragma unroll
-    for (int j = 0; j < RG; j++) v[j] = (b0 + j < nblocks) ? partial[(size_t)(b0 + j) * SLAB + p] : 0.0f;
+    float4 v[RG];
 #pragma unroll
     for (int j = 0; j < RG; j++)
-      if (b0 + j < nblocks) acc = acc + v[j];
+      v[j] = (b0 + j < nblocks) ? ((const float4*)(partial + (size_t)(b0 + j) * SLAB))[q]
+                                : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int j = 0; j < RG; j++)
+      if (b0 + j < nblocks) {
+        acc.x = acc.x + v[j].x; acc.y = acc.y + v[j].y;
+        acc.z = acc.z + v[j].z; acc.w = acc.w + v[j].w;
+      }
   }
-  gs[gi][pi] = acc;
+  gs[gi][qi] = acc;
   __syncthreads();
-  if (gi == 0 && p < SLAB) {
+  if (gi < 4 && q < SLAB / 4) {  // one parameter per thread: component gi of quad qi
+    const float* gf = (const float*)gs;
+    const int p = 4 * q + gi;
     float t = 0.0f;
-    for (int g = 0; g < ngroups; g++) t = t + gs[g][pi];
+    for (int g = 0; g < ngroups; g++) t = t + gf[(g * 16 + qi) * 4 + gi];
     grad[p] = t;
     if (ADAM && p < NPARAM) adam_param(a, p, t);
   }
@@ -438,7 +447,7 @@ hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t 
 hipError_t launch_grad_reduce(const float* partial, int nblocks, float* part2, float* grad,
                               hipStream_t s) {
   if (nblocks <= RG * RG) {
-    hipLaunchKernelGGL(k_grad_reduce_fused<false>, dim3((SLAB + 15) / 16), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_grad_reduce_fused<false>, dim3((SLAB / 4 + 15) / 16), dim3(256), 0, s,
                        partial, nblocks, grad, AdamArgs{});
     return hipGetLastError();
   }
@@ -452,7 +461,7 @@ int grad_reduce_groups(int nblocks) { return (nblocks + RG - 1) / RG; }
 hipError_t launch_grad_reduce_adam(const float* partial, int nblocks, float* part2, float* grad,
                                    const AdamArgs& a, hipStream_t s) {
   if (nblocks <= RG * RG) {
-    hipLaunchKernelGGL(k_grad_reduce_fused<true>, dim3((SLAB + 15) / 16), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_grad_reduce_fused<true>, dim3((SLAB / 4 + 15) / 16), dim3(256), 0, s,
                        partial, nblocks, grad, a);
     return hipGetLastError();
   }
