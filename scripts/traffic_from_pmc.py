@@ -16,7 +16,7 @@ def read(path, name):
     counter summed over its per-unit rows"""
     per = {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == name and "k_env_side<true, true, false>" in r["Kernel_Name"]:
+        if r["Counter_Name"] == name and "k_env_side<true, true, false" in r["Kernel_Name"]:
             per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return sum(per.values()) / len(per), len(per)
 
