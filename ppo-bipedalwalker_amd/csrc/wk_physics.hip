@@ -394,9 +394,21 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   Body bA{A.cx, A.cy, &dA, mA.im, mA.ii};
   Body bB{B.cx, B.cy, &dB, mB.im, mB.ii};
   V2 rA, rB, rAF, rBF;
-  float j = calc_impulse(bA, bB, contact, 1.0f + e, n, rA, rB);
   V2 tangent = mk(-n.y, n.x);
-  float jf = calc_impulse(bA, bB, contact, mu, tangent, rAF, rBF);
+  float j, jf;
+  if constexpr (H == 2) {  // the normal impulse on half 0, the friction impulse on half 1
+    const uint32_t hm = sub ? 0xffffffffu : 0u;
+    const float mine = calc_impulse(bA, bB, contact, fsel(hm, mu, 1.0f + e),
+                                    mk(fsel(hm, tangent.x, n.x), fsel(hm, tangent.y, n.y)), rA, rB);
+    const float other = hswap(mine);
+    j = fsel(hm, other, mine);
+    jf = fsel(hm, mine, other);
+    rAF = rA;  // (the lever arms do not depend on the direction)
+    rBF = rB;
+  } else {
+    j = calc_impulse(bA, bB, contact, 1.0f + e, n, rA, rB);
+    jf = calc_impulse(bA, bB, contact, mu, tangent, rAF, rBF);
+  }
   if (TRACE && tr && pi >= 0) { tr->impulse[pi][0] = j; tr->impulse[pi][1] = jf; }
   apply_impulses<BSTATIC>(bA, bB, n, j, rA, rB);
   apply_impulses<BSTATIC>(bA, bB, tangent, jf, rAF, rBF);
