@@ -325,17 +325,21 @@ __global__ void k_grad_reduce2_adam(const float* __restrict__ part2, int ngroups
 }
 
 // One-launch form of the two stages for nblocks <= RG * RG, bit-identical association
-// (RG consecutive slabs in order, then the groups in order): a block owns 16 parameter
+// (RG consecutive slabs in order, then the groups in order): a block owns QB parameter
 // quads; thread (group gi, quad qi) folds its group's RG slabs with 16-byte loads (all issued
 // before the ordered adds), and the 16 group sums are folded in order through LDS.  ADAM: the
 // single-GPU tail applies Adam as well.
+#ifndef WK_REDUCE_QB
+#define WK_REDUCE_QB 16
+#endif
+enum { QB = WK_REDUCE_QB };  // parameter quads per block (RG x QB threads; 16 timed best of 4 / 8 / 16)
 template <bool ADAM>
-__global__ __launch_bounds__(256) void k_grad_reduce_fused(const float* __restrict__ partial,
-                                                           int nblocks, float* grad, AdamArgs a) {
+__global__ __launch_bounds__(RG * QB) void k_grad_reduce_fused(const float* __restrict__ partial,
+                                                              int nblocks, float* grad, AdamArgs a) {
   static_assert(SLAB % 4 == 0, "16-byte slab rows");
-  __shared__ float4 gs[RG][16];
-  const int qi = threadIdx.x & 15, gi = threadIdx.x >> 4;
-  const int q = blockIdx.x * 16 + qi;  // parameters 4q .. 4q + 3
+  __shared__ float4 gs[RG][QB];
+  const int qi = threadIdx.x % QB, gi = threadIdx.x / QB;
+  const int q = blockIdx.x * QB + qi;  // parameters 4q .. 4q + 3
   const int ngroups = (nblocks + RG - 1) / RG;
   float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (q < SLAB / 4 && gi < ngroups) {
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(256) void k_grad_reduce_fused(const float* __restri
     const float* gf = (const float*)gs;
     const int p = 4 * q + gi;
     float t = 0.0f;
-    for (int g = 0; g < ngroups; g++) t = t + gf[(g * 16 + qi) * 4 + gi];
+    for (int g = 0; g < ngroups; g++) t = t + gf[(g * QB + qi) * 4 + gi];
     grad[p] = t;
     if (ADAM && p < NPARAM) adam_param(a, p, t);
   }
@@ -447,7 +451,7 @@ hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t 
 hipError_t launch_grad_reduce(const float* partial, int nblocks, float* part2, float* grad,
                               hipStream_t s) {
   if (nblocks <= RG * RG) {
-    hipLaunchKernelGGL(k_grad_reduce_fused<false>, dim3((SLAB / 4 + 15) / 16), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_grad_reduce_fused<false>, dim3((SLAB / 4 + QB - 1) / QB), dim3(RG * QB), 0, s,
                        partial, nblocks, grad, AdamArgs{});
     return hipGetLastError();
   }
@@ -461,7 +465,7 @@ int grad_reduce_groups(int nblocks) { return (nblocks + RG - 1) / RG; }
 hipError_t launch_grad_reduce_adam(const float* partial, int nblocks, float* part2, float* grad,
                                    const AdamArgs& a, hipStream_t s) {
   if (nblocks <= RG * RG) {
-    hipLaunchKernelGGL(k_grad_reduce_fused<true>, dim3((SLAB / 4 + 15) / 16), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_grad_reduce_fused<true>, dim3((SLAB / 4 + QB - 1) / QB), dim3(RG * QB), 0, s,
                        partial, nblocks, grad, a);
     return hipGetLastError();
   }
