@@ -736,10 +736,10 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
           for (int d = 0; d < 4; d++) {
             const f4 w3 = *(const f4*)(lds + W3 + d * 64 + 16 * M + 4 * g);
 #pragma unroll
-            for (int r = 0; r < 4; r++) p3[d] = p3[d] + w3[r] * h2[M][r];
+            for (int r = 0; r < 4; r++) p3[d] = __builtin_fmaf(w3[r], h2[M][r], p3[d]);
           }
 #pragma unroll
-          for (int r = 0; r < 4; r++) pv = pv + wc2[r] * hc1[M][r];
+          for (int r = 0; r < 4; r++) pv = __builtin_fmaf(wc2[r], hc1[M][r], pv);
         }
 #pragma unroll
         for (int d = 0; d < 4; d++) {
@@ -808,7 +808,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
             awc2[M][r] = __builtin_fmaf(criticLoss, hc1[M][r], awc2[M][r]);
             float gh = 0.0f;
 #pragma unroll
-            for (int d = 0; d < 4; d++) gh = gh + w3[d][r] * q[d];
+            for (int d = 0; d < 4; d++) gh = __builtin_fmaf(w3[d][r], q[d], gh);
             gz2[r] = gh * mf_dlrelu(h2[M][r]);
             gzc1[r] = (0.0f + wc2[r] * criticLoss) * mf_dlrelu(hc1[M][r]);
           }
