@@ -49,8 +49,10 @@ static_assert(LDS_FLOATS >= WAVES * SLAB, "the epilogue's per-wave slabs fit");
 }  // namespace mf
 
 // ActivationLayer LeakyReLU(0.2) = Math.Max(0.2 z, z): z for z >= 0 (and -0: Max keeps
-// the equal-valued 0.2 * -0 = -0), 0.2 z below, NaN through -- a select, no branches
-DEV float mf_lrelu(float z) { return z < 0.0f ? 0.2f * z : z; }
+// the equal-valued 0.2 * -0 = -0), 0.2 z below, NaN through.  As v_max_f32(0.2 z, z) it is the
+// same value for every input (0.2 z is NaN exactly when z is, has z's sign, and is the larger
+// one exactly when z < 0): two instructions instead of multiply, compare and select.
+DEV float mf_lrelu(float z) { return __builtin_fmaxf(0.2f * z, z); }
 DEV float mf_dlrelu(float z) { return z < 0.0f ? 0.2f : 1.0f; }
 DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
