@@ -20,6 +20,16 @@
 #include "wk_kernels.h"
 #include "wk_mfma_layout.h"
 
+// Build parts (the Makefile compiles this file three times, in parallel): kernels are
+// templates instantiated where the host shims at the end launch them, so each part holds the
+// shims of one family -- 1: the pair / quad side kernels, 2 and 4: the scene-prop kernel
+// (given actions / policy), 3: the rest (1- and 16-lane kernels, the counting replay, init,
+// obs, policy, returns).  0: all.
+#ifndef WK_PHYS_PART
+#define WK_PHYS_PART 0
+#endif
+#define WK_PART(k) (WK_PHYS_PART == 0 || WK_PHYS_PART == (k))
+
 #ifndef WK_ENV_WAVES
 #define WK_ENV_WAVES 2
 #endif
@@ -34,7 +44,7 @@ namespace wk {
 // Optional per-region wave-time profile (build with -DWK_REGION_PROF; scripts/region_prof.py):
 // s_memtime deltas accumulated per wave, summed over waves into g_region_prof.
 #ifdef WK_REGION_PROF
-__device__ unsigned long long g_region_prof[16];
+static __device__ unsigned long long g_region_prof[16];  // (probe builds; read in part 1)
 struct RegionProf { uint64_t acc[8]; uint64_t t; };
 DEV void rp_mark(RegionProf* p, int r) {
   if (p) { const uint64_t t = __builtin_amdgcn_s_memtime(); p->acc[r] += t - p->t; p->t = t; }
@@ -1279,6 +1289,7 @@ void k_env_side(EnvParams P, StepArgs A) {
 }
 
 // env initialisation: Environment ctor (Environment.cs:39-51) -- episode-0 body order
+#if WK_PART(3)
 __global__ void k_env_init(EnvParams P, float* st, const float* dxoff, const uint8_t* mask,
                            int post) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1357,11 +1368,14 @@ __global__ void k_returns(int n, int T, int use_gae, float gamma, float lambda,
   }
 }
 
+#endif  // WK_PART(3)
 }  // namespace wk
 
+#if WK_PART(2) || WK_PART(4)
 namespace wk {
 #include "wk_scene.inc"
 }  // namespace wk
+#endif
 
 // host-side launch shims (C++ linkage, used by wk_api.cpp)
 namespace wk {
@@ -1380,6 +1394,7 @@ static void launch_lanes(int mode, const EnvParams& P, const StepArgs& A, hipStr
   if (P.rough) launch_lanes_floor<L, true>(mode, P, A, s);
   else launch_lanes_floor<L, false>(mode, P, A, s);
 }
+#if WK_PART(1)
 template <int Q>
 static void launch_side(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
   dim3 blk(SIDE_BLOCK), grd((unsigned)(((size_t)P.n_env * 2 * Q + SIDE_BLOCK - 1) / SIDE_BLOCK));
@@ -1390,15 +1405,36 @@ static void launch_side(int mode, const EnvParams& P, const StepArgs& A, hipStre
     default: hipLaunchKernelGGL((k_env_side<true, true, false, Q>), grd, blk, 0, s, P, A); break;
   }
 }
-hipError_t launch_env_scene(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
+void launch_side_pair(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) { launch_side<1>(mode, P, A, s); }
+void launch_side_quad(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) { launch_side<2>(mode, P, A, s); }
+#endif
+#if WK_PART(2)
+void launch_env_scene_given(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
                             hipStream_t s) {
   dim3 blk(64), grd((unsigned)((P.n_env + 63) / 64));
-  switch (mode) {
-    case 0: hipLaunchKernelGGL((k_env_scene<false, false, false>), grd, blk, 0, s, P, A, S); break;
-    case 1: hipLaunchKernelGGL((k_env_scene<false, false, true>), grd, blk, 0, s, P, A, S); break;
-    case 2: hipLaunchKernelGGL((k_env_scene<true, false, false>), grd, blk, 0, s, P, A, S); break;
-    default: hipLaunchKernelGGL((k_env_scene<true, true, false>), grd, blk, 0, s, P, A, S); break;
-  }
+  if (mode == 0) hipLaunchKernelGGL((k_env_scene<false, false, false>), grd, blk, 0, s, P, A, S);
+  else hipLaunchKernelGGL((k_env_scene<false, false, true>), grd, blk, 0, s, P, A, S);
+}
+#endif
+#if WK_PART(4)
+void launch_env_scene_policy(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
+                             hipStream_t s) {
+  dim3 blk(64), grd((unsigned)((P.n_env + 63) / 64));
+  if (mode == 2) hipLaunchKernelGGL((k_env_scene<true, false, false>), grd, blk, 0, s, P, A, S);
+  else hipLaunchKernelGGL((k_env_scene<true, true, false>), grd, blk, 0, s, P, A, S);
+}
+#endif
+#if WK_PART(3)
+void launch_side_pair(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s);
+void launch_side_quad(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s);
+void launch_env_scene_given(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
+                            hipStream_t s);
+void launch_env_scene_policy(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
+                             hipStream_t s);
+hipError_t launch_env_scene(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
+                            hipStream_t s) {
+  if (mode <= 1) launch_env_scene_given(mode, P, A, S, s);
+  else launch_env_scene_policy(mode, P, A, S, s);
   return hipGetLastError();
 }
 hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
@@ -1408,13 +1444,14 @@ hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipS
     hipLaunchKernelGGL((k_env_step<false, false, false, 1, false, true>), grd, blk, 0, s, P, A);
     return hipGetLastError();
   }
-  if (P.lanes == 2) launch_side<1>(mode, P, A, s);
-  else if (P.lanes == 4) launch_side<2>(mode, P, A, s);
+  if (P.lanes == 2) launch_side_pair(mode, P, A, s);
+  else if (P.lanes == 4) launch_side_quad(mode, P, A, s);
   else if (P.lanes == 16) launch_lanes<16>(mode, P, A, s);
   else launch_lanes<1>(mode, P, A, s);
   return hipGetLastError();
 }
-#ifdef WK_REGION_PROF
+#endif  // WK_PART(3)
+#if defined(WK_REGION_PROF) && WK_PART(1)
 extern "C" int wk_region_prof(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_region_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
   if (reset) {
@@ -1424,6 +1461,7 @@ extern "C" int wk_region_prof(unsigned long long* out, int reset) {
   return 0;
 }
 #endif
+#if WK_PART(3)
 hipError_t launch_env_init(const EnvParams& P, float* st, const float* dx, const uint8_t* mask,
                            int post, hipStream_t s) {
   hipLaunchKernelGGL(k_env_init, dim3((P.n_env + 255) / 256), dim3(256), 0, s, P, st, dx, mask, post);
@@ -1447,4 +1485,5 @@ hipError_t launch_returns(int n, int T, int use_gae, float gamma, float lambda, 
                      lambda, r, v, d, ret, adv);
   return hipGetLastError();
 }
+#endif  // WK_PART(3)
 }  // namespace wk
