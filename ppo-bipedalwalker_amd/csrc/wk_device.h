@@ -315,7 +315,8 @@ DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, 
       proj_minmax(Q, axis.x, axis.y, qmin, qmax);
     }
     const float temp = __builtin_fminf(qmax - pmin, pmax - qmin);
-    sep = sep || (valid && !(temp > 0.0f));
+    // (no per-axis separation flag: an axis separates iff !(temp > 0), and depth ends as the
+    // minimum temp over the valid axes, so the callers test depth > 0 once -- see sat())
     const bool take = valid && temp < depth;
     depth = take ? temp : depth;
     normal.x = take ? axis.x : normal.x;
@@ -332,8 +333,7 @@ DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, 
 DEV void floor_axis(float pmin, float pmax, float qmin, float qmax, float nx, float ny, bool& sep,
                     V2& normal, float& depth) {
   const float temp = __builtin_fminf(qmax - pmin, pmax - qmin);
-  sep = sep || !(temp > 0.0f);
-  const bool take = temp < depth;  // see axis_pass
+  const bool take = temp < depth;  // see axis_pass (separation: the caller's depth > 0)
   depth = take ? temp : depth;
   normal.x = take ? nx : normal.x;
   normal.y = take ? ny : normal.y;
@@ -351,7 +351,7 @@ DEV bool sat_floor(const Poly<NA>& A, const Poly<4>& F, float mnx, float mny, fl
   floor_axis(-1050.0f, -900.0f, -mxy, -mny, -0.0f, -1.0f, sep, normal, depth);
   V2 dir = mk(F.cx - A.cx, F.cy - A.cy);
   if (vdot(dir, normal) > 0.0f) normal = vmul(normal, -1.0f);
-  return !sep;
+  return depth > 0.0f;  // (see sat)
 }
 
 template <int NA, int NB, bool BZE = false>
@@ -364,7 +364,11 @@ DEV bool sat(const Poly<NA>& A, const Poly<NB>& B, V2& normal, float& depth,
   axis_pass<NB, NA, false, BZE>(B, A, sep, normal, depth, AXB);
   V2 dir = mk(B.cx - A.cx, B.cy - A.cy);
   if (vdot(dir, normal) > 0.0f) normal = vmul(normal, -1.0f);
-  return !sep;
+  // AxisChecks returns false at the first axis whose projections do not overlap, i.e. with
+  // !(temp > 0) (verdict algebra in axis_pass).  depth is the minimum temp over every valid
+  // axis (take = temp < depth), so for a finite state "no axis separates" is exactly
+  // depth > 0 -- one compare here instead of one per axis.
+  return depth > 0.0f;
 }
 
 // ---------------- SAT, axes split over an L-lane row (L in {4, 8, 16}) ----------------

@@ -249,7 +249,6 @@ DEV bool sat_split(const Poly<N>& A, const Poly<N>& B, int half, V2& normal, flo
   V2 nn = mk(0.0f, 0.0f);
   float dd = FLT_MAX;
   axis_pass<N, N, false, false>(P, Q, sep, nn, dd, &AXP);
-  const bool sep_o = hswap(sep ? 1.0f : 0.0f) != 0.0f;
   const float dd_o = hswap(dd), nx_o = hswap(nn.x), ny_o = hswap(nn.y);
   const float dA = half ? dd_o : dd, dB = half ? dd : dd_o;
   const V2 nA = half ? mk(nx_o, ny_o) : nn, nB = half ? nn : mk(nx_o, ny_o);
@@ -258,7 +257,7 @@ DEV bool sat_split(const Poly<N>& A, const Poly<N>& B, int half, V2& normal, flo
   normal = takeB ? nB : nA;
   const V2 dir = mk(B.cx - A.cx, B.cy - A.cy);
   if (vdot(dir, normal) > 0.0f) normal = vmul(normal, -1.0f);
-  return !(sep || sep_o);
+  return depth > 0.0f;  // (no axis separates: see sat in wk_device.h)
 }
 // GetContactPoints with the two faces split: half 0 A's on the normal, half 1 B's on its
 // negation (each from its own SAT axes), exchanged, then the clipping in both
@@ -293,14 +292,12 @@ DEV bool sat_floor_split(const Poly<6>& A, const Poly<4>& F, float mnx, float mn
   float dd = FLT_MAX;
   EdgeAxes<6> own;
   axis_pass<6, 4, true, false, 3>(R, F, sep, nn, dd, &own);
-  const bool sep_o = hswap(sep ? 1.0f : 0.0f) != 0.0f;
   const float dd_o = hswap(dd), nx_o = hswap(nn.x), ny_o = hswap(nn.y);
   const float d0 = half ? dd_o : dd, d1 = half ? dd : dd_o;
   const V2 n0 = half ? mk(nx_o, ny_o) : nn, n1 = half ? nn : mk(nx_o, ny_o);
   const bool take1 = d1 < d0;
   depth = take1 ? d1 : d0;
   normal = take1 ? n1 : n0;
-  sep = sep || sep_o;
 #pragma unroll
   for (int i = 0; i < 3; i++) {
     const float ox = hswap(own.x[i]), oy = hswap(own.y[i]);
@@ -315,7 +312,7 @@ DEV bool sat_floor_split(const Poly<6>& A, const Poly<4>& F, float mnx, float mn
   floor_axis(-1050.0f, -900.0f, -mxy, -mny, -0.0f, -1.0f, sep, normal, depth);
   V2 dir = mk(F.cx - A.cx, F.cy - A.cy);
   if (vdot(dir, normal) > 0.0f) normal = vmul(normal, -1.0f);
-  return !sep;
+  return depth > 0.0f;  // (see sat in wk_device.h)
 }
 
 // RigidBody.ResolveCollisions body for one (this=A, other=B) candidate
