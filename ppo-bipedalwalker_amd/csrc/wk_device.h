@@ -627,6 +627,51 @@ DEV int contact_points_ax(const Poly<NA>& A, const EdgeAxes<NA>& AXA, const Poly
   significant_face_ax(B, AXB, vneg(normal), ia, ib, imax, id);
   return contact_clip(ra, rb, rmax, rd, ia, ib, imax, id, normal, c0, c1);
 }
+// significant_face_ax(floor_poly, floor_axes(), n) for the flat floor box, vertices
+// (-50,1050), (-50,900), (1050,900), (1050,1050): the same four projections and first strict
+// minimum, then the vertex, its neighbours and the two axes are constants selected by the
+// index's two bits (b1 b0) instead of ten bit-select chains -- the same values whenever a
+// minimum exists (a NaN normal, already a fault, takes index 0).
+DEV void floor_face_ax(V2 n, V2& fa, V2& fb, V2& fmax, V2& fdir) {
+  const float xa = -50.0f * n.x, xb = 1050.0f * n.x, ya = 1050.0f * n.y, yb = 900.0f * n.y;
+  const float p[4] = {xa + ya, xa + yb, xb + yb, xb + ya};
+  float mind = FLT_MAX;
+  bool b0 = false, b1 = false;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const bool lt = p[i] < mind;
+    mind = lt ? p[i] : mind;
+    b0 = lt ? (i & 1) != 0 : b0;
+    b1 = lt ? (i >> 1) != 0 : b1;
+  }
+  const bool bx = b0 != b1;
+  const V2 sig = mk(b1 ? 1050.0f : -50.0f, bx ? 900.0f : 1050.0f);  // vertex idx
+  const V2 va = mk(bx ? 1050.0f : -50.0f, b1 ? 1050.0f : 900.0f);   // vertex idx + 1
+  const V2 vb = mk(bx ? -50.0f : 1050.0f, b1 ? 900.0f : 1050.0f);   // vertex idx - 1
+  const float ex = b0 ? -0.0f : (b1 ? -1.0f : 1.0f), ey = b0 ? (b1 ? -1.0f : 1.0f) : 0.0f;
+  const float px = b0 ? (b1 ? -1.0f : 1.0f) : -0.0f, py = b0 ? 0.0f : (b1 ? 1.0f : -1.0f);
+  const V2 after = mk(-ey, ex);
+  const V2 before = mk(py, -px);
+  const bool first = vdot(n, before) >= vdot(n, after);
+  fa = first ? sig : va;
+  fb = first ? vb : sig;
+  fmax = sig;
+  fdir = first ? vneg(before) : after;
+}
+template <int NA>
+DEV int contact_points_floor(const Poly<NA>& A, const EdgeAxes<NA>& AXA, V2 normal, V2& c0,
+                             V2& c1) {
+  V2 ra, rb, rmax, rd, ia, ib, imax, id;
+  significant_face_ax(A, AXA, normal, ra, rb, rmax, rd);
+#if WK_FLOOR_FACE_LOOP
+  Poly<4> F;
+  floor_poly(F);
+  significant_face_ax(F, floor_axes(), vneg(normal), ia, ib, imax, id);
+#else
+  floor_face_ax(vneg(normal), ia, ib, imax, id);
+#endif
+  return contact_clip(ra, rb, rmax, rd, ia, ib, imax, id, normal, c0, c1);
+}
 
 template <int NA, int NB, bool SAFE = false>
 DEV int contact_points(const Poly<NA>& A, const Poly<NB>& B, V2 normal, V2& c0, V2& c1) {

@@ -369,7 +369,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   V2 c0, c1;
   int nc;
   if constexpr (H == 2 && !BSTATIC) nc = contacts_split(own, axa, sub, n, c0, c1);
-  else if constexpr (KEEP && FLAT) nc = contact_points_ax(A, axa, B, floor_axes(), n, c0, c1);
+  else if constexpr (KEEP && FLAT) nc = contact_points_floor(A, axa, n, c0, c1);
   else if constexpr (KEEP) nc = contact_points_ax(A, axa, B, axb, n, c0, c1);
   else nc = contact_points<NA, NB, GENERIC>(A, B, n, c0, c1);
   rp_mark(rp, RP_CONTACT);
