@@ -371,9 +371,25 @@ def test_fast_sqrt_rcp_exhaustive():
     assert "0 mismatches" in r.stdout
 
 
+def test_floor_face_closed_form():
+    """The flat floor's contact face from the argmin index bits (floor_face_ax) equals the
+    generic significant_face_ax over the floor polygon bit for bit, for 2^26 hashed normals
+    and every pair of 24 special components (tests/cpp/floor_face_check.hip)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "ppo-bipedalwalker_amd", "build", "floor_face_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(os.path.dirname(exe)), "check"],
+                       check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 mismatches" in r.stdout
+
+
 def test_baseline_config2_physics_4096(wk, orc):
-    """BASELINE config 2: 4,096 walkers, physics-step only (auto mapping = the 2-lane leg
-    split at every size), 10 env-steps with given actions, bit-exact vs the oracle."""
+    """BASELINE config 2: 4,096 walkers, physics-step only (auto mapping: the quad split at
+    this size), 10 env-steps with given actions, bit-exact vs the oracle."""
     n, k = 4096, 10
     eng = wk.Engine(n, seed=SEED, RandomizeStart=1)
     assert eng.cfg.LanesPerWalker == 0
