@@ -120,6 +120,9 @@ def lib():
             "orc_train_trajectory": (None, [C.c_void_p, C.POINTER(Hyper), U64, C.c_uint32, I, C.c_void_p,
                                             C.c_void_p, C.c_void_p, C.c_void_p]),
             "orc_train_episode_seconds": (C.c_double, [C.POINTER(Hyper), U64, I]),
+            "orc_replay_batch": (I, [C.POINTER(Hyper), I, I, P, P, P, P, P, P, P]),
+            "orc_perm_batch": (None, [U32, U32, P, P]),
+            "orc_env_setup_batch": (None, [U64, I, I, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -325,6 +328,40 @@ def perm_key(seed, update, epoch):
 
 def perm(i, n, key):
     return lib().orc_perm(int(i), int(n), _p(np.ascontiguousarray(key, np.uint32)))
+
+
+def perm_batch(count, n, key):
+    """orc_perm(i, n, key) for i < count (OpenMP)"""
+    out = np.empty(int(count), np.uint32)
+    lib().orc_perm_batch(int(count), int(n), _p(np.ascontiguousarray(key, np.uint32)), _p(out))
+    return out.astype(np.int64)
+
+
+def env_setup(seed, n, first=0):
+    """(dx[n], material[n]) of RandomizeStart / RandomizeMaterial for walkers first..first+n-1"""
+    dx = np.empty(int(n), np.float32)
+    mat = np.empty(int(n), np.int32)
+    lib().orc_env_setup_batch(int(seed), int(first), int(n), _p(dx), _p(mat))
+    return dx, mat
+
+
+def replay_batch(actions, dx=None, mat=None, **hkw):
+    """n walkers from the episode-0 template (offsets dx, materials mat) stepped T env-steps
+    with actions[T][n][4] in C (OpenMP over walkers).  Returns (obs_before[T][n][12],
+    rewards[T][n], dones[T][n], final records[n][112])."""
+    a = np.ascontiguousarray(actions, np.float32)
+    T, n = a.shape[0], a.shape[1]
+    h = hyper(**hkw)
+    obs = np.empty((T, n, 12), np.float32)
+    rew = np.empty((T, n), np.float32)
+    done = np.empty((T, n), np.uint8)
+    dump = np.empty((n, STATE_FLOATS), np.float32)
+    dxa = None if dx is None else np.ascontiguousarray(dx, np.float32)
+    ma = None if mat is None else np.ascontiguousarray(mat, np.int32)
+    if lib().orc_replay_batch(C.byref(h), n, T, _p(dxa), _p(ma), _p(a), _p(obs), _p(rew),
+                              _p(done), _p(dump)) != 0:
+        raise MemoryError("orc_replay_batch")
+    return obs, rew, done, dump
 
 
 def kat_pole_floor(vy):

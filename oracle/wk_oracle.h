@@ -172,6 +172,13 @@ void orc_train_trajectory(orc_agent* ag, const orc_hyper* h, uint64_t seed, uint
 int orc_physics_loop(const orc_hyper* h, uint64_t seed, int env_id, int n_steps);
 double orc_train_episode_seconds(const orc_hyper* h, uint64_t seed, int T);
 
+/* batched drivers (orc_batch.c, OpenMP over independent walkers) */
+int orc_replay_batch(const orc_hyper* h, int n, int T, const float* dx, const int* mat,
+                     const float* actions, float* obs_before, float* reward, uint8_t* done,
+                     float* dump);
+void orc_perm_batch(uint32_t count, uint32_t n, const uint32_t key[4], uint32_t* out);
+void orc_env_setup_batch(uint64_t seed, int first, int n, float* dx, int* mat);
+
 #ifdef __cplusplus
 }
 #endif
