@@ -33,15 +33,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ppo-bipedalwalker_amd"))
 
 METRIC = "env-steps/sec (whole node) + PPO-update ms, 65k walkers at 1/2/4/8 MI355X"
-# MI355X_MICROARCH.md: fp32 vector peak 157.3 TF counts an FMA as 2 flops at the packed
-# (v_pk_fma_f32) rate.  The physics is restated op for op with no FMA contraction (parity),
-# so its honest ceilings are the packed mul/add rate (78.6 T flop/s) and, for the scalar
-# ops that dominate the dependent chains, the non-packed issue rate (39.3 T op/s:
-# 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz).
+# MI355X_MICROARCH.md: fp32 peak 157.3 TF (vector = matrix: v_mfma_f32_16x16x4_f32 runs at the
+# vector rate), i.e. 1,024 SIMDs x 2.4 GHz x 64 flop/clk -- a wave64 v_fma_f32 (128 flop) every
+# 2 cycles.  The physics is restated op for op with no FMA contraction (parity), so one VALU
+# instruction is one flop per lane: its ceiling is the scalar non-FMA rate, 78.6 T op/s
+# (a wave64 instruction per 2 cycles per SIMD), reachable once each SIMD holds >= 2 waves.
+# With one wave per SIMD a wave issues one VALU instruction per 4 cycles (the guide's
+# 'vector-instruction ISSUE cost' row): 39.3 T, scaled by the share of SIMDs that hold a wave.
 PEAK_FP32_TFLOPS = 157.3
-PEAK_NOFMA_PACKED = 78.6
-PEAK_NOFMA_SCALAR = 39.3
+PEAK_NOFMA = 78.6
+PEAK_NOFMA_ONE_WAVE = 39.3
+N_SIMDS = 1024
 PEAK_HBM_GBS = 8000.0
+# SURVEY 8(d) PPO-update flop model: per sample and epoch, forward + backward of actor and
+# critic (PPOAgent.cs:218-346, DenseLayer.cs:103-120); Adam ~14 flop x 6,149 per minibatch
+FLOP_GRAD_SAMPLE = 36569
+FLOP_ADAM_MINIBATCH = 86086
+SLAB_BYTES = 6152 * 4  # gradient + 3 diagnostics, padded to 16 B: the all-reduce payload
 # SURVEY.md 8(d) flop model, priced per counted physics event (wk_count_events):
 FLOP_INTEGRATE = 477          # per walker-substep: 4 poles x 95 + hull 81 + floor 16
 FLOP_JOINT = 107              # per Joint.Step past the 0.1 early-out ((2x106 + 2x108) / 4)
@@ -79,6 +87,8 @@ def parse():
                    help="skip the configs 2 / 3 / 4-shard / 5-shard lines (N = 1 only)")
     p.add_argument("--cpu-baseline-steps", type=int, default=150000)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="processes of the all-cores CPU baseline (0: every CPU the process may use)")
     p.add_argument("--rehearse", action="store_true",
                    help="multi-rank rehearsal on ONE GPU: every rank on device 0, gradients "
                         "all-reduced on the host over gloo (wk_comm_init_host) instead of RCCL "
@@ -126,6 +136,24 @@ def _cpu_model():
     return "unknown"
 
 
+def _cpu_quota():
+    """CPUs the cgroup grants this process (cgroup v2 cpu.max, v1 cfs quota), or None"""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_baseline(args):
     """the oracle (C restatement of the reference's single-threaded C#
     loop) on the host cores: (i) 1 walker on 1 core -- the full loop (policy + physics +
@@ -147,7 +175,14 @@ def cpu_baseline(args):
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    threads = max(1, min(16, avail))  # the box's CPU share for one GPU is 16
+    # one walker per process on every CPU this process may run on: the affinity set, capped by
+    # the cgroup's CPU quota when it has one (more processes than granted CPUs only time-share)
+    quota = _cpu_quota()
+    threads = max(1, min(avail, int(quota)) if quota else avail)
+    if args.cpu_threads:
+        threads = args.cpu_threads
+    why = (f"affinity {avail} CPUs" + (f", cgroup quota {quota:g} CPUs" if quota else ", no cgroup quota")
+           + (" (overridden by --cpu-threads)" if args.cpu_threads else ""))
     n_each = max(1000, n // 4)
     all_rate = _all_cores(threads, n_each, args.seed)
     return {"value": n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
@@ -158,11 +193,45 @@ def cpu_baseline(args):
             "train_ms_per_1001_step_episode": train_ms,
             "all_cores": {"threads": threads, "env_steps_per_s": all_rate,
                           "sample": f"{threads} processes x {n_each} env-steps of the reference loop",
-                          "nproc": os.cpu_count(), "affinity_cpus": avail,
-                          "cpu_model": _cpu_model()}}
+                          "nproc": os.cpu_count(), "affinity_cpus": avail, "cgroup_cpu_quota": quota,
+                          "threads_reason": why, "cpu_model": _cpu_model()}}
 
 
 # ---------------------------------------------------------------- GPU -------------------
+def valu_ceiling(lanes_per_walker, walkers):
+    """the non-FMA VALU ceiling of a rollout launch: 2+ waves per SIMD -> 78.6 T; else one
+    wave per SIMD on the share of SIMDs that hold one (MI355X_MICROARCH.md issue-cost row)"""
+    waves = -(-lanes_per_walker * walkers // 64)
+    if waves >= 2 * N_SIMDS:
+        return PEAK_NOFMA, "scalar non-FMA fp32 issue, >= 2 waves per SIMD"
+    return (PEAK_NOFMA_ONE_WAVE * min(1.0, waves / N_SIMDS),
+            f"one wave per SIMD on {min(waves, N_SIMDS)} of {N_SIMDS} SIMDs "
+            "(a wave64 VALU instruction per 4 cycles)")
+
+
+def update_roofline(prof_k, samples_per_minibatch, walkers, horizon, epochs, update_ms):
+    """SURVEY 8(d) update roofline: the gradient kernel (k_ppo_grad_ws, one launch per
+    minibatch) priced at 36,569 flop per sample over its mean HIP-event launch time, and the
+    whole update (gradient + reduction + Adam over all minibatches) over its measured time"""
+    launches = max(1, prof_k.get("grad_launches", 0))
+    grad_us = prof_k["grad_ms"] / launches * 1e3
+    achieved = FLOP_GRAD_SAMPLE * samples_per_minibatch / (grad_us * 1e-6) / 1e12
+    n_mb = epochs * (walkers * horizon // samples_per_minibatch)
+    upd_flop = epochs * walkers * horizon * FLOP_GRAD_SAMPLE + n_mb * FLOP_ADAM_MINIBATCH
+    upd_tf = upd_flop / (update_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "kernel": "k_ppo_grad_ws (producer/consumer v_mfma_f32_16x16x4_f32)",
+            "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
+            "samples_per_launch": samples_per_minibatch, "flop_per_sample": FLOP_GRAD_SAMPLE,
+            "mean_launch_us": grad_us, "launches": launches,
+            "reduce_adam_us": prof_k["reduce_ms"] / max(1, prof_k.get("reduce_launches", 0)) * 1e3,
+            "update": {"minibatches": n_mb, "flop": upd_flop, "ms": update_ms,
+                       "achieved": upd_tf, "frac": upd_tf / PEAK_FP32_TFLOPS},
+            "note": ("achieved = 36,569 flop/sample (SURVEY 8(d)) x samples per launch / mean "
+                     "gradient-kernel launch time (HIP events on the engine stream, one untimed "
+                     "profiled iteration)")}
+
+
 def flops_per_env_step(ev):
     """SURVEY 8(d)'s per-primitive constants priced on the counted events"""
     f = FLOP_INTEGRATE * ev["substeps"] + FLOP_JOINT * ev["joint"] + FLOP_IMPULSE * (
@@ -224,15 +293,42 @@ def extra_config(wk, torch, args, n, M, M_global, horizon, physics_only=False, m
         dt = time_iterations(eng, args, k, horizon, args.regime_iters)
         prof = eng.profile()
         eng.profile_enable(0)
+        eng.profile_reset()
+        eng.profile_enable(2)  # untimed: an event pair around every launch of one iteration
+        time_iterations(eng, args, 1, horizon, args.regime_iters)
+        eng.profile_enable(0)
+        prof_k = eng.profile()
+        upd_ms = prof["update_ms"] / max(1, prof["update_calls"])
         return {"walkers": n, "minibatch": M, "minibatch_global": M_global,
                 "env_steps_per_s": k * n * horizon / dt,
                 "rollout_ms": prof["physics_ms"] / max(1, prof["physics_launches"]),
                 "rollout_env_steps_per_s": n * horizon * prof["physics_launches"]
                 / max(1e-9, prof["physics_ms"] * 1e-3),
-                "ppo_update_ms": prof["update_ms"] / max(1, prof["update_calls"]),
-                "minibatches_per_update": args.epochs * (n * horizon // M)}
+                "ppo_update_ms": upd_ms,
+                "minibatches_per_update": args.epochs * (n * horizon // M),
+                "roofline_update": update_roofline(prof_k, M, n, horizon, args.epochs, upd_ms)}
     finally:
         eng.close()
+
+
+def allreduce_one_rank(wk, eng, args, horizon, update_index):
+    """the collective path on one GPU -- a one-rank RCCL communicator makes
+    wk_ppo_update run ordered reduction -> ncclAllReduce (24.6 KB, on the engine stream) ->
+    Adam per minibatch, as every rank of the multi-GPU run does; one untimed profiled
+    iteration gives the mean RCCL call time (a one-rank all-reduce moves no data over xGMI:
+    a lower bound on the N > 1 exchange's latency)"""
+    eng.comm_init(0, 1, wk.Engine.comm_unique_id())
+    eng.profile_reset()
+    eng.profile_enable(2)
+    time_iterations(eng, args, 2, horizon, update_index)
+    eng.profile_enable(0)
+    p = eng.profile()
+    calls = max(1, p["allreduce_calls"])
+    return {"bytes": SLAB_BYTES, "calls": p["allreduce_calls"],
+            "ms_per_call": p["allreduce_ms"] / calls,
+            "ms_per_update": p["allreduce_ms"] / 2, "update_ms": p["update_ms"] / 2,
+            "kernel_ms_one_step": {k: v / 2 for k, v in p.items() if k.endswith("_ms")},
+            "note": "one-rank RCCL communicator on this GPU: the collective path of every rank"}
 
 
 def main():
@@ -334,6 +430,7 @@ def main():
             traffic = None
     # the mapping wk_create picks (include/wk_api.h, LanesPerWalker 0 = auto)
     lanes = args.lanes or (4 if shard.n_local <= 16384 else 2)
+    ceiling, ceiling_why = valu_ceiling(lanes, shard.n_local)
     kernel = {2: "k_env_side<true,true,false,1>", 4: "k_env_side<true,true,false,2> (quad mapping)",
               16: "k_env_step<true,true,false,16,false>",
               1: "k_env_step<true,true,false,1,false>"}[lanes]
@@ -376,10 +473,9 @@ def main():
             "unit": "TFLOP/s",
             "frac": achieved / PEAK_FP32_TFLOPS,
             "traffic": traffic,
-            "peak_no_fma_packed": PEAK_NOFMA_PACKED,
-            "frac_no_fma_packed": achieved / PEAK_NOFMA_PACKED,
-            "peak_no_fma_scalar_issue": PEAK_NOFMA_SCALAR,
-            "frac_no_fma_scalar_issue": achieved / PEAK_NOFMA_SCALAR,
+            "peak_no_fma": ceiling,
+            "frac_no_fma": achieved / ceiling,
+            "peak_no_fma_basis": ceiling_why,
             "flop_per_env_step_counted": f_counted,
             "flop_per_env_step_upper_bound": FLOP_UPPER,
             "events_per_env_step": {k: v / ev["env_steps"] for k, v in ev.items()
@@ -394,7 +490,11 @@ def main():
                      "events on the engine stream)"),
         },
         "kernel_ms_one_step": {k: v for k, v in prof_k.items() if k.endswith("_ms")},
+        "roofline_update": update_roofline(prof_k, shard.minibatch_local, shard.n_local, T,
+                                           args.epochs, upd_ms_max / args.steps),
     }
+    if world == 1 and not args.rehearse:
+        out["allreduce_1rank"] = allreduce_one_rank(wk, eng, args, T, upd)
     if rank == 0 and world == 1 and not args.no_extras:
         ex = {}
         ex["config2_physics_4096"] = extra_config(wk, torch, args, 4096, 4096, 4096, T,

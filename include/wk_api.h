@@ -249,12 +249,15 @@ int wk_step(wk_ctx* ctx, const float* actions_or_null /* k*n_env*4, unclipped */
  * the step (_trajectory.States, :73), the sampled UNCLIPPED action (Walker.GetActions ->
  * PPOAgent.SampleActions, :74 / PPOAgent.cs:381-398; recorded at :86), its per-dimension
  * log-probability (:74, :87), the reward (:88) and terminal flag, the critic value of the
- * state (GetValueEstimate, PPOAgent.cs:447-456) and the next state (post-reset after a
- * terminal step).  Any output may be NULL.  Layouts [k][n_env][...]. */
+ * state (GetValueEstimate, PPOAgent.cs:447-456), the next state (post-reset after a
+ * terminal step) and the torso position after the step, BEFORE any auto-reset
+ * (Walker.GetPosition as Step reads it for _bestDistance, Environment.cs:113-119).  Any
+ * output may be NULL.  Layouts [k][n_env][...]. */
 int wk_step_sampled(wk_ctx* ctx, int k_steps, float* states /* k*n*12 */,
                     float* actions /* k*n*4 */, float* logp /* k*n*4 */,
                     float* values /* k*n */, float* reward /* k*n */, uint8_t* done /* k*n */,
-                    float* next_obs /* k*n*12 */, uint32_t* fault /* n */);
+                    float* next_obs /* k*n*12 */, uint32_t* fault /* n */,
+                    float* position /* k*n*2 */);
 int wk_step_device(wk_ctx* ctx, const float* d_actions_or_null, int k_steps, float* d_obs,
                    float* d_reward, uint8_t* d_done, uint32_t* d_fault);
 /* one env-step with per-substep pair bookkeeping: trace[n_env * Iterations] */
@@ -370,7 +373,11 @@ int wk_allreduce_test(wk_ctx* ctx, float* host_buf, int n); /* sum in place (tes
  * ordered reduction each minibatch's slab (gradient + diagnostics, n floats) is copied to the
  * host, fn must replace it in place with the sum over ranks (return 0), and it is copied back
  * before Adam.  For hosts without RCCL (MPI, a CPU control plane) and for testing the
- * multi-rank path of several processes sharing one GPU (RCCL refuses duplicate devices). */
+ * multi-rank path of several processes sharing one GPU (RCCL refuses duplicate devices).
+ * fn is kept for the context's lifetime (a managed caller must keep its delegate alive).  A
+ * non-zero return fails this rank's wk_ppo_update with WK_ERR_COMM mid-update (no Adam step
+ * for that minibatch) while the peers wait in their own all-reduce: it is fatal for the
+ * whole job -- abort every rank. */
 typedef int (*wk_host_allreduce_fn)(float* buf, int n, void* user);
 int wk_comm_init_host(wk_ctx* ctx, int rank, int nranks, wk_host_allreduce_fn fn, void* user);
 

@@ -84,6 +84,8 @@ def lib():
             "orc_env_prop": (I, [P, I, P, P]),
             "orc_env_step": (None, [P, P, P, fp, C.POINTER(C.c_int), P]),
             "orc_env_get_obs": (None, [P, P]),
+            "orc_env_step_position": (None, [P, P]),
+            "orc_env_load": (None, [P, P]),
             "orc_env_dump": (None, [P, P]),
             "orc_env_reset": (None, [P]),
             "orc_env_set_torques": (None, [P, P]),
@@ -183,10 +185,20 @@ class Env:
         lib().orc_env_get_obs(self.p, _p(o))
         return o
 
+    def step_position(self):
+        """torso position after the last step, before its auto-reset (Environment.cs:119)"""
+        o = np.empty(2, np.float32)
+        lib().orc_env_step_position(self.p, _p(o))
+        return o
+
     def dump(self):
         s = np.empty(STATE_FLOATS, np.float32)
         lib().orc_env_dump(self.p, _p(s))
         return s
+
+    def load(self, state):
+        """inverse of dump(): start from a given walker state record"""
+        lib().orc_env_load(self.p, _p(np.ascontiguousarray(state, np.float32)))
 
     def reset(self):
         lib().orc_env_reset(self.p)

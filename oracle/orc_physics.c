@@ -93,6 +93,7 @@ struct orc_env {
   int rough;
   joint joints[4];
   v2 position, prev_position;
+  v2 step_position;    /* position after the last Step, before any Reset (Environment.cs:119) */
   int terminal;
   int steps, episodes, post_reset;
   int material;
@@ -750,6 +751,7 @@ void orc_env_step(orc_env* e, const float action[4], float obs[12], float* rewar
     terminal = 1;
   }
   orc_env_get_obs(e, obs);
+  e->step_position = e->position;  /* _bestDistance reads it here (Environment.cs:119) */
   if (terminal) {
     e->episodes++;
     orc_env_reset(e);
@@ -757,6 +759,11 @@ void orc_env_step(orc_env* e, const float action[4], float obs[12], float* rewar
   }
   *reward_out = reward;
   *done_out = terminal;
+}
+
+void orc_env_step_position(const orc_env* e, float out[2]) {
+  out[0] = e->step_position.x;
+  out[1] = e->step_position.y;
 }
 
 void orc_env_dump(const orc_env* e, float out[ORC_STATE_FLOATS]) {
@@ -785,6 +792,31 @@ void orc_env_dump(const orc_env* e, float out[ORC_STATE_FLOATS]) {
   out[ORC_ST_POSTRESET] = (float)e->post_reset;
   out[ORC_ST_TERMINAL] = (float)e->terminal;
   out[ORC_ST_EPISODES] = (float)e->episodes;
+}
+
+/* the inverse of orc_env_dump for the walker (flat-floor or rough env): vertices,
+ * centroids, velocities, angles, Collided, torques, positions, counters and the body order
+ * (materials / inertia stay the env's).  Test infrastructure: lets a test start the oracle
+ * from a state the GPU context was given (wk_set_state). */
+void orc_env_load(orc_env* e, const float in[ORC_STATE_FLOATS]) {
+  for (int b = 0; b < ORC_NB; b++) {
+    body* bd = &e->bodies[b];
+    const float* o = in + b * ORC_BODY_STRIDE;
+    for (int i = 0; i < bd->nv; i++) bd->v[i] = V(o[2 * i], o[2 * i + 1]);
+    bd->centroid = V(o[12], o[13]);
+    bd->lin_vel = V(o[14], o[15]);
+    bd->ang_vel = o[16];
+    bd->angle = o[17];
+    bd->collided = o[18] != 0.0f;
+  }
+  for (int j = 0; j < 4; j++) e->joints[j].torque = in[ORC_ST_TORQUE + j];
+  e->position = V(in[ORC_ST_POS], in[ORC_ST_POS + 1]);
+  e->prev_position = V(in[ORC_ST_PREV], in[ORC_ST_PREV + 1]);
+  e->steps = (int)in[ORC_ST_STEPS];
+  e->post_reset = in[ORC_ST_POSTRESET] != 0.0f;
+  e->terminal = in[ORC_ST_TERMINAL] != 0.0f;
+  e->episodes = (int)in[ORC_ST_EPISODES];
+  build_order(e);
 }
 
 /* K3: an axis-aligned Carpet pole centred at (125, 874.75) -- bottom edge

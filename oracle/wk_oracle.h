@@ -108,6 +108,10 @@ int orc_env_prop(const orc_env* e, int k, float* xy, float st[6]);
 void orc_env_step(orc_env* e, const float action[4], float obs[12], float* reward,
                   int* done, orc_pair_trace* trace);
 void orc_env_get_obs(const orc_env* e, float obs[12]);
+/* torso position after the last orc_env_step, before its auto-reset (Environment.cs:119) */
+void orc_env_step_position(const orc_env* e, float out[2]);
+/* inverse of orc_env_dump (walker bodies, counters, body order) */
+void orc_env_load(orc_env* e, const float in[ORC_STATE_FLOATS]);
 void orc_env_dump(const orc_env* e, float out[ORC_STATE_FLOATS]);
 void orc_env_reset(orc_env* e);
 /* substep-level hooks for unit tests */

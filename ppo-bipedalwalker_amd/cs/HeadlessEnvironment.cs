@@ -34,6 +34,9 @@ public sealed class HeadlessEnvironment : IDisposable
     float _bestDistance = 0;
     float _previousAverageReward = 0;
 
+    // Hyperparameters.CollectData: ConsoleRenderer.AddTotalEpisodeReward / AddCriticLoss /
+    // AddActorLoss only append when it is set (ConsoleRenderer.cs:79-95)
+    public bool CollectData { get; set; } = true;
     public List<float> TotalRewards { get; } = new();  // ConsoleRenderer._totalRewards
     public List<float> CriticLosses { get; } = new();  // ConsoleRenderer._criticLosses
     public List<float> ActorLosses { get; } = new();   // ConsoleRenderer._actorLosses
@@ -55,7 +58,7 @@ public sealed class HeadlessEnvironment : IDisposable
         InitialState();
     }
 
-    public void Dispose() => Wk.wk_destroy(_ctx);
+    public void Dispose() => Wk.Destroy(_ctx);
 
     // InitialState (:175-180): Walker.Update + GetState
     public void InitialState()
@@ -75,8 +78,9 @@ public sealed class HeadlessEnvironment : IDisposable
         var r = new float[1];
         var d = new byte[1];
         var next = new float[WkConst.Obs];
+        var pos = new float[2];
         // deltaTime: the context steps with its configured DeltaTime (Game1's fixed step)
-        if (!Wk.Ok(_ctx, Wk.wk_step_sampled(_ctx, 1, s, a, lp, v, r, d, next, null),
+        if (!Wk.Ok(_ctx, Wk.wk_step_sampled(_ctx, 1, s, a, lp, v, r, d, next, null, pos),
                    "Exception occurred during the environment update", _log))
             return;
         _trajectory.States.Add(s);             // == _state (:73)
@@ -85,9 +89,10 @@ public sealed class HeadlessEnvironment : IDisposable
         _trajectory.Rewards.Add(r[0]);         // (:88)
         _trajectory.Values.Add(v[0]);
         _state = next;
-        float x = GetPosition().x;
-        if (x > _bestDistance) _bestDistance = x;  // Step (:119)
-        if (d[0] != 0) TrainNetworks();            // the context has already reset the walker
+        // Step (:119) reads the position after the step and before Reset: the context has
+        // already re-created a terminal walker, so the pre-reset position comes from the step
+        if (pos[0] > _bestDistance) _bestDistance = pos[0];
+        if (d[0] != 0) TrainNetworks();
     }
 
     // TrainNetworks (:157-164) -> Walker.Train -> PPOAgent.Train(Trajectory) (PPOAgent.cs:147-172)
@@ -96,7 +101,7 @@ public sealed class HeadlessEnvironment : IDisposable
         _episodes++;
         _previousAverageReward = _trajectory.Rewards.Average();
         int T = _trajectory.Rewards.Count;
-        TotalRewards.Add((float)_trajectory.Rewards.Sum(x => (double)x));  // PPOAgent.cs:151
+        if (CollectData) TotalRewards.Add((float)_trajectory.Rewards.Sum(x => (double)x));  // PPOAgent.cs:151
         var S = _trajectory.States.SelectMany(x => x).ToArray();
         var A = _trajectory.Actions.SelectMany(x => x).ToArray();
         var L = _trajectory.LogProbabilities.SelectMany(x => x).ToArray();
@@ -104,17 +109,23 @@ public sealed class HeadlessEnvironment : IDisposable
         var V = _trajectory.Values.ToArray();
         var D = new byte[T];
         D[T - 1] = 1;                          // one episode: returns restart after it
-        if (Wk.Ok(_ctx, Wk.wk_set_trajectory(_ctx, T, S, A, L, R, D, V), "Exception while storing the trajectory", _log))
+        // PPOAgent.cs:153-166: valueLoss / actorLoss start at 0 and keep the last minibatch's
+        // diagnostics; with floor(T / BatchSize) == 0 minibatches no Train(Batch) runs and the
+        // zeros are appended all the same
+        float critic = 0, actor = 0;
+        if (Wk.Ok(_ctx, Wk.wk_set_trajectory(_ctx, T, S, A, L, R, D, V), "Exception while storing the trajectory", _log)
+            && T >= _cfg.BatchSize)
         {
             var args = new WkPpoArgs { Epochs = _cfg.Epochs, Minibatch = _cfg.BatchSize,
                                        MinibatchGlobal = _cfg.BatchSize, UpdateIndex = (uint)(_episodes - 1) };
-            if (T >= _cfg.BatchSize &&
-                Wk.Ok(_ctx, Wk.wk_ppo_update(_ctx, ref args, out float critic, out float actor),
-                      "Exception while training the networks", _log))
-            {
-                CriticLosses.Add(critic);      // ConsoleRenderer.AddCriticLoss (PPOAgent.cs:165)
-                ActorLosses.Add(actor);        // ConsoleRenderer.AddActorLoss (:166)
-            }
+            if (!Wk.Ok(_ctx, Wk.wk_ppo_update(_ctx, ref args, out critic, out actor),
+                       "Exception while training the networks", _log))
+                critic = actor = 0;
+        }
+        if (CollectData)
+        {
+            CriticLosses.Add(critic);          // ConsoleRenderer.AddCriticLoss (PPOAgent.cs:165)
+            ActorLosses.Add(actor);            // ConsoleRenderer.AddActorLoss (:166)
         }
         Reset();
     }

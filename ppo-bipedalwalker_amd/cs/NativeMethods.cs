@@ -152,7 +152,7 @@ public static class Wk
     [DllImport(Lib)] public static extern int wk_set_materials(IntPtr ctx, int[] matId);
     [DllImport(Lib)] public static extern int wk_set_offsets(IntPtr ctx, float[] dx);
     [DllImport(Lib)] public static extern int wk_step(IntPtr ctx, float[]? actions, int kSteps, float[]? obs, float[]? reward, byte[]? done, uint[]? fault);
-    [DllImport(Lib)] public static extern int wk_step_sampled(IntPtr ctx, int kSteps, float[]? states, float[]? actions, float[]? logp, float[]? values, float[]? reward, byte[]? done, float[]? nextObs, uint[]? fault);
+    [DllImport(Lib)] public static extern int wk_step_sampled(IntPtr ctx, int kSteps, float[]? states, float[]? actions, float[]? logp, float[]? values, float[]? reward, byte[]? done, float[]? nextObs, uint[]? fault, float[]? position);
     [DllImport(Lib)] public static extern int wk_step_device(IntPtr ctx, IntPtr dActions, int kSteps, IntPtr dObs, IntPtr dReward, IntPtr dDone, IntPtr dFault);
     [DllImport(Lib)] public static extern int wk_step_traced(IntPtr ctx, float[] actions, [Out] WkPairTrace[] trace);
     [DllImport(Lib)] public static extern int wk_get_obs(IntPtr ctx, float[] obs);
@@ -206,6 +206,25 @@ public static class Wk
     [DllImport(Lib)] public static extern int wk_allreduce_test(IntPtr ctx, float[] buf, int n);
     [UnmanagedFunctionPointer(CallingConvention.Cdecl)] public delegate int HostAllReduce(IntPtr buf, int n, IntPtr user);
     [DllImport(Lib)] public static extern int wk_comm_init_host(IntPtr ctx, int rank, int nRanks, HostAllReduce fn, IntPtr user);
+
+    // libwk keeps the function pointer for the context's lifetime; the marshalled thunk dies with
+    // the delegate, so the delegate must stay reachable until the context is destroyed.  Use
+    // CommInitHost / Destroy instead of the raw entry points when a host all-reduce is set.
+    // A failing callback (non-zero return) fails that rank's wk_ppo_update with WK_ERR_COMM
+    // while its peers wait in their own all-reduce: treat it as fatal for the whole job.
+    static readonly System.Collections.Concurrent.ConcurrentDictionary<IntPtr, HostAllReduce> s_hostAllReduce = new();
+    public static int CommInitHost(IntPtr ctx, int rank, int nRanks, HostAllReduce fn, IntPtr user)
+    {
+        int rc = wk_comm_init_host(ctx, rank, nRanks, fn, user);
+        if (rc == 0) s_hostAllReduce[ctx] = fn;
+        return rc;
+    }
+    public static int Destroy(IntPtr ctx)
+    {
+        int rc = wk_destroy(ctx);
+        s_hostAllReduce.TryRemove(ctx, out _);
+        return rc;
+    }
 
     // profiling, counting replay, snapshots
     [DllImport(Lib)] public static extern int wk_profile_enable(IntPtr ctx, int on);

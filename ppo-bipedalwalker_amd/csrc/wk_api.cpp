@@ -511,7 +511,8 @@ int wk_step(wk_ctx* c, const float* actions, int k, float* obs, float* reward, u
 }
 
 int wk_step_sampled(wk_ctx* c, int k, float* states, float* actions, float* logp, float* values,
-                    float* reward, uint8_t* done, float* next_obs, uint32_t* fault) {
+                    float* reward, uint8_t* done, float* next_obs, uint32_t* fault,
+                    float* position) {
   DevGuard dg_(c);
   if (!c || k <= 0) return WK_ERR_ARG;
   const size_t n = c->n, kn = (size_t)k * n;
@@ -519,7 +520,8 @@ int wk_step_sampled(wk_ctx* c, int k, float* states, float* actions, float* logp
   // buffer of wk_rollout is not touched)
   const size_t b12 = sizeof(float) * 12 * kn, b4 = sizeof(float) * 4 * kn, b1 = sizeof(float) * kn;
   const size_t b_fault = sizeof(uint32_t) * n;
-  const size_t total = 2 * b12 + 2 * b4 + 2 * b1 + kn + b_fault + 8 * 64;
+  const size_t b_pos = sizeof(float) * 2 * kn;
+  const size_t total = 2 * b12 + 2 * b4 + 2 * b1 + kn + b_fault + b_pos + 9 * 64;
   if (ensure(c, &c->scratch2, &c->scratch2_bytes, total)) return WK_ERR_HIP;
   char* p = (char*)c->scratch2;
   auto take = [&](size_t bytes) { char* r = p; p += (bytes + 63) & ~(size_t)63; return r; };
@@ -530,11 +532,13 @@ int wk_step_sampled(wk_ctx* c, int k, float* states, float* actions, float* logp
   float* d_r = (float*)take(b1);
   float* d_o = (float*)take(b12);
   uint32_t* d_f = (uint32_t*)take(b_fault);
+  float* d_pos = (float*)take(b_pos);
   uint8_t* d_d = (uint8_t*)take(kn);
   HIPCHK(c, hipMemsetAsync(d_f, 0, b_fault, c->stream));
   wk::StepArgs A{};
   A.st = c->st; A.dxoff = c->dxoff; A.mat = c->mat; A.rng_t = c->rng_t;
   A.obs_out = next_obs ? d_o : nullptr; A.fault_out = d_f;
+  A.pos_out = position ? d_pos : nullptr;
   A.W = c->W; A.Wz = c->Wz; A.lp_const = c->lp_const;
   A.traj_s = d_s; A.traj_a = d_a; A.traj_lp = d_lp; A.traj_r = d_r; A.traj_d = d_d; A.traj_v = d_v;
   A.t0 = 0; A.k_steps = k;
@@ -550,6 +554,7 @@ int wk_step_sampled(wk_ctx* c, int k, float* states, float* actions, float* logp
   if (done) HIPCHK(c, hipMemcpyAsync(done, d_d, kn, hipMemcpyDeviceToHost, c->stream));
   if (next_obs) HIPCHK(c, hipMemcpyAsync(next_obs, d_o, b12, hipMemcpyDeviceToHost, c->stream));
   if (fault) HIPCHK(c, hipMemcpyAsync(fault, d_f, b_fault, hipMemcpyDeviceToHost, c->stream));
+  if (position) HIPCHK(c, hipMemcpyAsync(position, d_pos, b_pos, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return WK_OK;
 }
@@ -1523,15 +1528,22 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
     SETERR(c, "'%s' is not a wk checkpoint", path);
     return WK_ERR_ARG;
   }
-  // version 2 (before scene props) has no scene section, version 3 no CkptExt
-  const bool v2 = h.version == 2;
-  const size_t ext_bytes = h.version >= 4 ? sizeof(CkptExt) : 0;
-  CkptExt ext{0, 0, 0, 0};  // files before version 4 were flat-floor runs
-  if (ext_bytes && data.size() >= sizeof h + ext_bytes) memcpy(&ext, data.data() + sizeof h, sizeof ext);
-  size_t need = ckpt_bytes(n) + ext_bytes + (v2 ? 0 : sizeof(int32_t));
+  // version 2 (before scene props) has no scene section, version 3 no CkptExt.  Neither
+  // records RoughFloor (which already existed when they were written), and nothing in the
+  // walker records tells the floors apart: loading one could run the wrong physics on the
+  // saved walkers, so it is refused
+  if (h.version < 4) {
+    SETERR(c, "checkpoint '%s' is version %u: its floor type (RoughFloor) was not recorded "
+              "before version 4, so it cannot be resumed safely", path, h.version);
+    return WK_ERR_CONFIG;
+  }
+  const size_t ext_bytes = sizeof(CkptExt);
+  CkptExt ext{0, 0, 0, 0};
+  if (data.size() >= sizeof h + ext_bytes) memcpy(&ext, data.data() + sizeof h, sizeof ext);
+  size_t need = ckpt_bytes(n) + ext_bytes + sizeof(int32_t);
   int32_t np = 0;
   std::vector<wk_prop> desc;
-  if (!v2 && data.size() >= need) {
+  if (data.size() >= need) {
     memcpy(&np, data.data() + need - sizeof(int32_t), sizeof np);
     if (np < 0 || np > WK_MAX_PROPS) { SETERR(c, "checkpoint '%s': invalid scene section", path); return WK_ERR_ARG; }
     if (np > 0 && data.size() >= need + sizeof(wk_prop) * np) {
@@ -1582,7 +1594,7 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
   HIPCHK(c, hipMemcpy(c->mat, q, sizeof(int32_t) * n, hipMemcpyHostToDevice)); q += sizeof(int32_t) * n;
   HIPCHK(c, hipMemcpy(c->ep_acc, q, sizeof(double) * n, hipMemcpyHostToDevice)); q += sizeof(double) * n;
   HIPCHK(c, hipMemcpy(c->ep_len, q, sizeof(int32_t) * n, hipMemcpyHostToDevice)); q += sizeof(int32_t) * n;
-  if (np > 0) {  // (np > 0 only in a version-3+ file)
+  if (np > 0) {
     q += sizeof(int32_t) + sizeof(wk_prop) * np;
     HIPCHK(c, hipMemcpy(c->props, q, sizeof(float) * n * c->scene.pstride, hipMemcpyHostToDevice));
   }

@@ -78,15 +78,11 @@ DEV V2 vnormalize(V2 a) {
   return mk(a.x * val, a.y * val);
 }
 
-// System.Math.Min/Max(float, float) (IEEE 754:2019 minimum/maximum)
-DEV float net_minf(float x, float y) {
-  if (x != y) { if (!__builtin_isnan(x)) return x < y ? x : y; return x; }
-  return __builtin_signbit(x) ? x : y;
-}
-DEV float net_maxf(float x, float y) {
-  if (x != y) { if (!__builtin_isnan(x)) return y < x ? x : y; return x; }
-  return __builtin_signbit(y) ? x : y;
-}
+// System.Math.Min/Max(float, float) (IEEE 754:2019 minimum/maximum: a NaN operand gives
+// NaN, -0 < +0).  gfx950 has them as one instruction (v_minimum3_f32 / v_maximum3_f32); the
+// compare-and-select restatement (the oracle's net_minf) compiled to two branches.
+DEV float net_minf(float x, float y) { return __builtin_elementwise_minimum(x, y); }
+DEV float net_maxf(float x, float y) { return __builtin_elementwise_maximum(x, y); }
 
 // Matrix.Clip(m, 1, -1) (Walker/PPO/Matrix.cs:377-405)
 DEV float clip1(float x) {
@@ -283,8 +279,9 @@ DEV void proj_minmax(const Poly<N>& P, float ax, float ay, float& mn, float& mx)
 // likewise max): the box projects in 4 products, 2 min, 2 max, 2 adds instead of a
 // 4-vertex loop -- the same values (a zero's sign aside, which no overlapping axis sees).
 //
-// Verdict algebra (finite state; a non-finite state is already a fault): fl(a - b) > 0 iff
-// a > b, so the axis overlaps iff temp = min(qmax - pmin, pmax - qmin) > 0; and a depth or
+// Verdict algebra: fl(a - b) > 0 iff a > b, so a finite axis overlaps iff temp =
+// min(qmax - pmin, pmax - qmin) > 0, and a NaN temp (Math.Min propagates it; IsOverlapping's
+// compares are then false) separates and keeps depth NaN (see below); and a depth or
 // normal is only ever used when no axis separates, so an axis may be taken on temp < depth
 // alone -- whenever a separating axis exists the caller discards both.  ZE: P may have a
 // zero edge (a rough-floor segment); a walker polygon's rigid edges never vanish.
@@ -314,11 +311,14 @@ DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, 
       proj_minmax(P, axis.x, axis.y, pmin, pmax);
       proj_minmax(Q, axis.x, axis.y, qmin, qmax);
     }
-    const float temp = __builtin_fminf(qmax - pmin, pmax - qmin);
+    const float temp = net_minf(qmax - pmin, pmax - qmin);
     // (no per-axis separation flag: an axis separates iff !(temp > 0), and depth ends as the
-    // minimum temp over the valid axes, so the callers test depth > 0 once -- see sat())
+    // minimum temp over the valid axes, so the callers test depth > 0 once -- see sat()).
+    // depth is the NaN-propagating minimum (one instruction, like the select it replaces): a
+    // NaN temp -- a non-finite vertex, where IsOverlapping's compares are false and
+    // AxisChecks returns false -- leaves depth NaN and the verdict depth > 0 false
     const bool take = valid && temp < depth;
-    depth = take ? temp : depth;
+    depth = valid ? net_minf(depth, temp) : depth;
     normal.x = take ? axis.x : normal.x;
     normal.y = take ? axis.y : normal.y;
   }
@@ -332,9 +332,9 @@ DEV void axis_pass(const Poly<NP>& P, const Poly<NQ>& Q, bool& sep, V2& normal, 
 // AxisChecks needs no vertex loop.  Same verdict, normal and depth bits as sat().
 DEV void floor_axis(float pmin, float pmax, float qmin, float qmax, float nx, float ny, bool& sep,
                     V2& normal, float& depth) {
-  const float temp = __builtin_fminf(qmax - pmin, pmax - qmin);
+  const float temp = net_minf(qmax - pmin, pmax - qmin);
   const bool take = temp < depth;  // see axis_pass (separation: the caller's depth > 0)
-  depth = take ? temp : depth;
+  depth = net_minf(depth, temp);
   normal.x = take ? nx : normal.x;
   normal.y = take ? ny : normal.y;
 }

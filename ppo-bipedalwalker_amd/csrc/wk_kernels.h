@@ -44,6 +44,8 @@ struct StepArgs {
   uint32_t* rng_t;           // [n] per-env env-step counter (Philox counter)
   const float* actions;      // [k][n][4] or null (policy)
   float* obs_out;            // [k][n][12] or null
+  float* pos_out;            // [k][n][2] torso centroid after the step, before any auto-reset
+                             // (Walker.GetPosition at Environment.cs:119) or null
   float* rew_out;            // [k][n] or null
   uint8_t* done_out;         // [k][n] or null
   uint32_t* fault_out;       // [n] or null (OR-accumulated)

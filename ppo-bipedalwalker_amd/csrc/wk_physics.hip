@@ -253,7 +253,7 @@ DEV bool sat_split(const Poly<N>& A, const Poly<N>& B, int half, V2& normal, flo
   const float dA = half ? dd_o : dd, dB = half ? dd : dd_o;
   const V2 nA = half ? mk(nx_o, ny_o) : nn, nB = half ? nn : mk(nx_o, ny_o);
   const bool takeB = dB < dA;
-  depth = takeB ? dB : dA;
+  depth = net_minf(dA, dB);  // (a NaN on either half stays NaN: no collision, see axis_pass)
   normal = takeB ? nB : nA;
   const V2 dir = mk(B.cx - A.cx, B.cy - A.cy);
   if (vdot(dir, normal) > 0.0f) normal = vmul(normal, -1.0f);
@@ -296,7 +296,7 @@ DEV bool sat_floor_split(const Poly<6>& A, const Poly<4>& F, float mnx, float mn
   const float d0 = half ? dd_o : dd, d1 = half ? dd : dd_o;
   const V2 n0 = half ? mk(nx_o, ny_o) : nn, n1 = half ? nn : mk(nx_o, ny_o);
   const bool take1 = d1 < d0;
-  depth = take1 ? d1 : d0;
+  depth = net_minf(d0, d1);
   normal = take1 ? n1 : n0;
 #pragma unroll
   for (int i = 0; i < 3; i++) {
@@ -809,6 +809,10 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArg
       terminal = true;
     }
     if (!state_finite(s)) fault |= 1u;
+    if (A.pos_out && leader) {
+      A.pos_out[((size_t)k * n + e) * 2] = s.posx;
+      A.pos_out[((size_t)k * n + e) * 2 + 1] = s.posy;
+    }
     if (terminal) {
       int ep = s.episodes + 1;
       make_template(s, dx);
@@ -1249,6 +1253,10 @@ void k_env_side(EnvParams P, StepArgs A) {
       terminal = true;
     }
     if (!side_finite(s)) fault |= 1u;
+    if (A.pos_out && leader) {
+      A.pos_out[((size_t)k * n + e) * 2] = s.posx;
+      A.pos_out[((size_t)k * n + e) * 2 + 1] = s.posy;
+    }
     if (terminal) {
       int ep = s.episodes + 1;
       make_template_side(s, dx);

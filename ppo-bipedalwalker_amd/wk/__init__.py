@@ -191,7 +191,7 @@ def load_library(path=None):
         "wk_step": (I, [P, P, I, P, P, P, P]),
         "wk_step_device": (I, [P, P, I, P, P, P, P]),
         "wk_step_traced": (I, [P, P, P]),
-        "wk_step_sampled": (I, [P, I, P, P, P, P, P, P, P, P]),
+        "wk_step_sampled": (I, [P, I, P, P, P, P, P, P, P, P, P]),
         "wk_get_obs": (I, [P, P]),
         "wk_get_state": (I, [P, P]),
         "wk_set_state": (I, [P, P]),
@@ -257,6 +257,9 @@ def _f32(a, shape=None):
     if shape is not None:
         a = a.reshape(shape)
     return a
+
+
+WK_ERR_COMM = -4  # enum wk_status (include/wk_api.h)
 
 
 class WkError(RuntimeError):
@@ -365,7 +368,11 @@ class Engine:
     # -- plumbing --
     def _chk(self, rc, what):
         if rc != 0:
-            raise WkError(f"{what} failed ({rc}): {self.lib.wk_last_error(self.h).decode()}")
+            msg = f"{what} failed ({rc}): {self.lib.wk_last_error(self.h).decode()}"
+            if rc == WK_ERR_COMM and getattr(self, "_host_ar_error", None):
+                msg += f" [host all-reduce callback raised {self._host_ar_error}; fatal for the job]"
+                self._host_ar_error = None
+            raise WkError(msg)
 
     def close(self):
         if getattr(self, "h", None):
@@ -414,16 +421,18 @@ class Engine:
     def step_sampled(self, k=1):
         """Environment.Update with the agent's sampling (wk_step_sampled): the Trajectory
         entries of Environment.cs:70-89 -- states before each step, unclipped actions,
-        per-dimension log-probabilities, values, rewards, dones -- and the next states."""
+        per-dimension log-probabilities, values, rewards, dones -- the next states, and the
+        torso position after each step before any auto-reset (Environment.cs:113-119)."""
         n = self.n
         out = dict(states=np.empty((k, n, 12), np.float32), actions=np.empty((k, n, 4), np.float32),
                    logp=np.empty((k, n, 4), np.float32), values=np.empty((k, n), np.float32),
                    rewards=np.empty((k, n), np.float32), dones=np.empty((k, n), np.uint8),
-                   next_obs=np.empty((k, n, 12), np.float32), fault=np.empty(n, np.uint32))
+                   next_obs=np.empty((k, n, 12), np.float32), fault=np.empty(n, np.uint32),
+                   position=np.empty((k, n, 2), np.float32))
         self._chk(self.lib.wk_step_sampled(
             self.h, int(k), _ptr(out["states"]), _ptr(out["actions"]), _ptr(out["logp"]),
             _ptr(out["values"]), _ptr(out["rewards"]), _ptr(out["dones"]), _ptr(out["next_obs"]),
-            _ptr(out["fault"])), "wk_step_sampled")
+            _ptr(out["fault"]), _ptr(out["position"])), "wk_step_sampled")
         return out
 
     def step_device(self, d_actions, k, d_obs, d_rew, d_done, d_fault):
@@ -642,12 +651,19 @@ class Engine:
 
     def comm_init_host(self, rank, nranks, allreduce):
         """wk_comm_init_host: `allreduce(np.ndarray float32 view)` sums the slab over ranks in
-        place (e.g. torch.distributed over gloo); the callback object is kept alive here."""
+        place (e.g. torch.distributed over gloo); the callback object is kept alive here.
+        A callback that raises fails this rank's wk_ppo_update with WK_ERR_COMM while the
+        peers wait inside their own all-reduce: the WkError carries the exception's text and
+        must be treated as fatal for the whole job (let it propagate so the launcher tears the
+        process group down; the ranks' replicas have diverged)."""
+        self._host_ar_error = None
+
         def _cb(buf, n, user):
             try:
                 allreduce(np.ctypeslib.as_array(buf, shape=(n,)))
                 return 0
-            except Exception:  # noqa: BLE001 -- reported as WK_ERR_COMM by the library
+            except Exception as ex:  # noqa: BLE001 -- reported as WK_ERR_COMM by the library
+                self._host_ar_error = f"{type(ex).__name__}: {ex}"
                 return 1
         self._host_ar = HOST_ALLREDUCE_FN(_cb)
         self._chk(self.lib.wk_comm_init_host(self.h, int(rank), int(nranks), self._host_ar, None),

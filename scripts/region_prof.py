@@ -1,5 +1,5 @@
 """Per-region wave time of the side-split env-step kernel (build: make LIB=libwk_prof.so
-BUILD=build_prof EXTRA=-DWK_REGION_PROF).  python scripts/region_prof.py [walkers] [T]"""
+BUILD=build_prof EXTRA=-DWK_REGION_PROF).  python scripts/region_prof.py [walkers] [T] [lanes]"""
 import ctypes as C
 import os
 import sys
@@ -11,8 +11,9 @@ import wk  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+L = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 names = ["joint", "integrate", "aabb", "sat", "contact", "impulse+move", "policy", "other"]
-eng = wk.Engine(n, seed=20250905, Horizon=T, RandomizeStart=1, LanesPerWalker=2)
+eng = wk.Engine(n, seed=20250905, Horizon=T, RandomizeStart=1, LanesPerWalker=L)
 lib = eng.lib
 lib.wk_region_prof.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 buf = (C.c_ulonglong * 16)()
@@ -29,7 +30,7 @@ for mode in ("rollout", "physics"):
     eng.sync()
     lib.wk_region_prof(buf, 1)
     tot = sum(buf[i] for i in range(8))
-    waves = n * 2 // 64
+    waves = -(-n * L // 64)
     print(f"{mode}: total {tot / waves / (T * 50):.0f} ticks per wave-substep")
     for i in range(8):
         print(f"  {names[i]:14s} {100.0 * buf[i] / tot:6.2f} %  {buf[i] / waves / (T * 50):9.1f}")

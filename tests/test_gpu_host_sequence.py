@@ -30,7 +30,8 @@ def test_csharp_host_sequence_until_first_train(wk, orc):
     env = orc.Env()
     state = eng.get_obs()[0]
     np.testing.assert_array_equal(state, env.obs())
-    gstep, trained = 0, False
+    gstep, trained, short_episodes = 0, False, 0
+    total_rewards, critic_losses, actor_losses = [], [], []
     for episode in range(40):
         S, A, L, R, V = [], [], [], [], []
         for _ in range(1001):
@@ -43,6 +44,8 @@ def test_csharp_host_sequence_until_first_train(wk, orc):
             np.testing.assert_allclose(lp, olp, rtol=1e-5, atol=1e-5)
             _, r, d = env.step(a)  # the oracle steps the recorded (unclipped) action
             assert r == out["rewards"][0, 0] and d == out["dones"][0, 0], (episode, gstep)
+            # the position Step reads for _bestDistance: after the step, before the reset
+            np.testing.assert_array_equal(out["position"][0, 0], env.step_position())
             S.append(s); A.append(a); L.append(lp); R.append(r); V.append(out["values"][0, 0])
             state = out["next_obs"][0, 0]
             if d:
@@ -57,12 +60,26 @@ def test_csharp_host_sequence_until_first_train(wk, orc):
         eng.set_trajectory(col(S), col(A), col(L), col(R), dones, col(V))
         ag.train_trajectory(np.stack(S), np.stack(A), np.stack(L), np.asarray(R, np.float32),
                             SEED, episode)  # floor(T / 64) == 0 minibatches: no Adam step
+        total_rewards.append(np.float32(np.sum(np.asarray(R, np.float64))))  # PPOAgent.cs:151
         if T < 64:
+            # floor(T / 64) == 0 minibatches: the reference runs no Train(Batch) and still
+            # appends valueLoss = actorLoss = 0 (PPOAgent.cs:153-166, ConsoleRenderer.cs:85-94);
+            # wk_ppo_update refuses an empty minibatch sequence, so the host skips the call
+            # (HeadlessEnvironment.TrainNetworks) and appends the zeros itself
+            with pytest.raises(wk.WkError, match="larger than the pool"):
+                eng.ppo_update(epochs=5, minibatch=64, minibatch_global=64, update_index=episode)
+            critic_losses.append(0.0)
+            actor_losses.append(0.0)
             np.testing.assert_array_equal(eng.get_weights(), ag.params())
+            short_episodes += 1
             continue
-        eng.ppo_update(epochs=5, minibatch=64, minibatch_global=64, update_index=episode)
+        cd, ad = eng.ppo_update(epochs=5, minibatch=64, minibatch_global=64, update_index=episode)
+        critic_losses.append(cd)
+        actor_losses.append(ad)
+        assert len(critic_losses) == len(actor_losses) == len(total_rewards) == episode + 1
         np.testing.assert_allclose(eng.get_weights(), ag.params(), rtol=0, atol=5e-6)
         assert eng.get_adam()[2] == ag.adam()[2] == 5 * (T // 64)
         trained = True
         break  # later episodes sample from weights 5e-6 apart: no longer bit-comparable
     assert trained
+    assert short_episodes > 0  # the zero-loss case was exercised (the untrained walker falls fast)

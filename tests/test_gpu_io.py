@@ -123,9 +123,10 @@ def _downgrade(raw, version):
 
 
 @pytest.mark.parametrize("version", [2, 3])
-def test_checkpoint_older_versions_still_load(wk, tmp_path, version):
-    """version-2 (no scene section: the layout before scene props) and version-3 files (no
-    RoughFloor record) load into a flat-floor context and clear its scene"""
+def test_checkpoint_older_versions_refused(wk, tmp_path, version):
+    """version-2 (no scene section) and version-3 files (no CkptExt) do not record RoughFloor,
+    which existed when they were written, and the walker records cannot tell the floors apart:
+    they are refused and the context -- walkers, weights and scene -- is unchanged"""
     a = wk.Engine(64, seed=SEED, RandomizeStart=1)
     a.step(np.random.default_rng(1).uniform(-1, 1, (3, 64, 4)).astype(np.float32), k=3)
     ck = tmp_path / "v4.ckpt"
@@ -134,10 +135,12 @@ def test_checkpoint_older_versions_still_load(wk, tmp_path, version):
     old.write_bytes(_downgrade(ck.read_bytes(), version))
     b = wk.Engine(64, seed=SEED)
     b.set_scene([wk.make_prop()])
-    b.checkpoint_load(old)
-    np.testing.assert_array_equal(a.get_state(), b.get_state())
-    with pytest.raises(wk.WkError):
-        b.prop_view(0, 0)
+    s0, w0 = b.get_state(), b.get_weights()
+    with pytest.raises(wk.WkError, match="floor type"):
+        b.checkpoint_load(old)
+    np.testing.assert_array_equal(b.get_state(), s0)
+    np.testing.assert_array_equal(b.get_weights(), w0)
+    b.prop_view(0, 0)  # the scene is still there
     a.close()
     b.close()
 

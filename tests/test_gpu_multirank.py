@@ -74,3 +74,18 @@ def test_two_ranks_host_allreduce(tmp_path):
         assert float(r["ad"]) == np.float32(r0["ad_l"]) + np.float32(r1["ad_l"])
     np.testing.assert_array_equal(r0["w2"], r1["w2"])
     assert not np.array_equal(r0["state"], r1["state"])  # different shards
+
+
+def test_failing_host_allreduce_is_reported(wk):
+    """a host all-reduce callback that raises fails wk_ppo_update with WK_ERR_COMM,
+    and the error names the callback's exception (the caller must abort the job)"""
+    eng = wk.Engine(64, seed=20250905, Horizon=4, Minibatch=64, Epochs=1)
+
+    def broken(buf):
+        raise ConnectionError("peer 1 went away")
+
+    eng.comm_init_host(0, 1, broken)
+    eng.rollout(4)
+    with pytest.raises(wk.WkError, match="ConnectionError: peer 1 went away"):
+        eng.ppo_update(update_index=0)
+    eng.close()
