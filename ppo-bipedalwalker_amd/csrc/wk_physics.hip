@@ -680,11 +680,19 @@ DEV void policy_row(const EnvParams& P, const float* __restrict__ W, float lp_co
   wave_lds_sync();  // the slice is rewritten by the next env-step
 }
 
-DEV bool state_finite(const EnvState& s) {
+// WK_FAULT_NONFINITE: x * 0 is NaN exactly for a NaN or infinite x, so the sum over every
+// vertex, centroid and velocity of the walker stays 0 iff all are finite (once per env-step)
+template <int N>
+DEV float nonfinite_acc(const Poly<N>& p, const Dyn& d) {
   float acc = 0.0f;
 #pragma unroll
-  for (int i = 0; i < 6; i++) acc += s.lll.x[i] * 0.0f + s.llu.x[i] * 0.0f + s.rll.x[i] * 0.0f + s.rlu.x[i] * 0.0f;
-  acc += s.dbody.vx * 0.0f + s.dbody.vy * 0.0f + s.body.cx * 0.0f + s.body.cy * 0.0f;
+  for (int i = 0; i < N; i++) acc += p.x[i] * 0.0f + p.y[i] * 0.0f;
+  return acc + (p.cx * 0.0f + p.cy * 0.0f) + (d.vx * 0.0f + d.vy * 0.0f) + (d.w * 0.0f + d.th * 0.0f);
+}
+DEV bool state_finite(const EnvState& s) {
+  const float acc = nonfinite_acc(s.lll, s.dlll) + nonfinite_acc(s.llu, s.dllu) +
+                    nonfinite_acc(s.rll, s.drll) + nonfinite_acc(s.rlu, s.drlu) +
+                    nonfinite_acc(s.body, s.dbody);
   return acc == 0.0f;
 }
 
@@ -1013,11 +1021,8 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
   rp_mark(rp, RP_OTHER);
 }
 
-DEV bool side_finite(const SideState& s) {
-  float acc = 0.0f;
-#pragma unroll
-  for (int i = 0; i < 6; i++) acc += s.lo.x[i] * 0.0f + s.up.x[i] * 0.0f;
-  acc += s.dbody.vx * 0.0f + s.dbody.vy * 0.0f + s.body.cx * 0.0f + s.body.cy * 0.0f;
+DEV bool side_finite(const SideState& s) {  // this side's legs and the torso (see state_finite)
+  const float acc = nonfinite_acc(s.lo, s.dlo) + nonfinite_acc(s.up, s.dup) + nonfinite_acc(s.body, s.dbody);
   return acc == 0.0f;
 }
 
@@ -1045,7 +1050,7 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool wri
   constexpr int NT = 2 / Q;  // 16-walker tiles per wave
   const int lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4, wl = lane >> (Q == 2 ? 2 : 1);
   float* tile = pl;          // [32 walkers][16]: 12 observations
-  float* outs = pl + 512;    // [32 walkers][8]: z3[0..3], critic output
+  float* outs = pl + 512;    // [32 walkers][8]: z3[0..3], critic output (disjoint from tile)
   if (writer) {
 #pragma unroll
     for (int q = 0; q < 3; q++) {
@@ -1054,92 +1059,73 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool wri
     }
   }
   wave_lds_sync();
-  float sB[NT][3];
-#pragma unroll
-  for (int nt = 0; nt < NT; nt++)
-#pragma unroll
-    for (int t = 0; t < 3; t++) sB[nt][t] = tile[(16 * nt + n) * 16 + 4 * t + g];
+  // one 16-walker tile at a time (not unrolled): a tile's layer-1 activations (16 VGPRs) are
+  // the only large live set, so the physics state around the call stays in registers
+  // (two tiles at once spilled ~56 VGPRs of the walker state per env-step at 65,536 walkers)
   const pf4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
-  pf4 h1[NT][4];
-  float pv[NT];
+#pragma unroll 1
+  for (int nt = 0; nt < NT; nt++) {
+    float sB[3];
 #pragma unroll
-  for (int nt = 0; nt < NT; nt++) pv[nt] = 0.0f;
+    for (int t = 0; t < 3; t++) sB[t] = tile[(16 * nt + n) * 16 + 4 * t + g];
+    pf4 h1[4];
+    float pv = 0.0f;
 #pragma unroll
-  for (int Mt = 0; Mt < 4; Mt++) {
-    float wa[3], wc[3];
+    for (int Mt = 0; Mt < 4; Mt++) {
+      float wa[3], wc[3];
 #pragma unroll
-    for (int t = 0; t < 3; t++) {
-      wa[t] = Wz[AW1F + (Mt * 3 + t) * 64 + lane];
-      wc[t] = Wz[CW1F + (Mt * 3 + t) * 64 + lane];
-    }
-    const pf4 ba = *(const pf4*)(Wz + BA1 + 16 * Mt + 4 * g);
-    const pf4 bc = *(const pf4*)(Wz + BC1 + 16 * Mt + 4 * g);
-    const pf4 w2c = *(const pf4*)(Wz + WC2 + 16 * Mt + 4 * g);
-#pragma unroll
-    for (int nt = 0; nt < NT; nt++) {
+      for (int t = 0; t < 3; t++) {
+        wa[t] = Wz[AW1F + (Mt * 3 + t) * 64 + lane];
+        wc[t] = Wz[CW1F + (Mt * 3 + t) * 64 + lane];
+      }
+      const pf4 ba = *(const pf4*)(Wz + BA1 + 16 * Mt + 4 * g);
+      const pf4 bc = *(const pf4*)(Wz + BC1 + 16 * Mt + 4 * g);
+      const pf4 w2c = *(const pf4*)(Wz + WC2 + 16 * Mt + 4 * g);
       pf4 acc = z4, accc = z4;
 #pragma unroll
       for (int t = 0; t < 3; t++) {
-        acc = pmfma(wa[t], sB[nt][t], acc);
-        accc = pmfma(wc[t], sB[nt][t], accc);
+        acc = pmfma(wa[t], sB[t], acc);
+        accc = pmfma(wc[t], sB[t], accc);
       }
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        h1[nt][Mt][r] = plrelu(acc[r] + ba[r]);
-        pv[nt] = pv[nt] + w2c[r] * plrelu(accc[r] + bc[r]);
+        h1[Mt][r] = plrelu(acc[r] + ba[r]);
+        pv = pv + w2c[r] * plrelu(accc[r] + bc[r]);
       }
     }
-  }
-  float p3[NT][4];
-#pragma unroll
-  for (int nt = 0; nt < NT; nt++)
-#pragma unroll
-    for (int d = 0; d < 4; d++) p3[nt][d] = 0.0f;
+    float p3[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 1
-  for (int Mt = 0; Mt < 4; Mt++) {  // not unrolled: keeps one Mt's weights in flight
-    pf4 acc[NT];
+    for (int Mt = 0; Mt < 4; Mt++) {  // not unrolled: keeps one Mt's weights in flight
+      pf4 acc = z4;
 #pragma unroll
-    for (int nt = 0; nt < NT; nt++) acc[nt] = z4;
+      for (int Mp = 0; Mp < 4; Mp++) {
+        const pf4 w = *(const pf4*)(Wz + W2F + ((Mt * 4 + Mp) * 64 + lane) * 4);
 #pragma unroll
-    for (int Mp = 0; Mp < 4; Mp++) {
-      const pf4 w = *(const pf4*)(Wz + W2F + ((Mt * 4 + Mp) * 64 + lane) * 4);
+        for (int r = 0; r < 4; r++) acc = pmfma(w[r], h1[Mp][r], acc);
+      }
+      const pf4 b2 = *(const pf4*)(Wz + BA2 + 16 * Mt + 4 * g);
 #pragma unroll
-      for (int r = 0; r < 4; r++)
+      for (int r = 0; r < 4; r++) {
+        const int k = 16 * Mt + 4 * g + r;
+        const float h2 = plrelu(acc[r] + b2[r]);
 #pragma unroll
-        for (int nt = 0; nt < NT; nt++) acc[nt] = pmfma(w[r], h1[nt][Mp][r], acc[nt]);
-    }
-    const pf4 b2 = *(const pf4*)(Wz + BA2 + 16 * Mt + 4 * g);
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int k = 16 * Mt + 4 * g + r;
-#pragma unroll
-      for (int nt = 0; nt < NT; nt++) {
-        const float h2 = plrelu(acc[nt][r] + b2[r]);
-#pragma unroll
-        for (int d = 0; d < 4; d++) p3[nt][d] = p3[nt][d] + Wz[W3 + d * 64 + k] * h2;
+        for (int d = 0; d < 4; d++) p3[d] = p3[d] + Wz[W3 + d * 64 + k] * h2;
       }
     }
-  }
-#pragma unroll
-  for (int nt = 0; nt < NT; nt++) {
 #pragma unroll
     for (int d = 0; d < 4; d++) {
-      p3[nt][d] = p3[nt][d] + __shfl_xor(p3[nt][d], 16);
-      p3[nt][d] = p3[nt][d] + __shfl_xor(p3[nt][d], 32);
+      p3[d] = p3[d] + __shfl_xor(p3[d], 16);
+      p3[d] = p3[d] + __shfl_xor(p3[d], 32);
     }
-    pv[nt] = pv[nt] + __shfl_xor(pv[nt], 16);
-    pv[nt] = pv[nt] + __shfl_xor(pv[nt], 32);
-  }
-  wave_lds_sync();  // the tile reads above are done before the outputs reuse LDS
-  if (g == 0) {
-#pragma unroll
-    for (int nt = 0; nt < NT; nt++) {
-      const pf4 v = {p3[nt][0], p3[nt][1], p3[nt][2], p3[nt][3]};
+    pv = pv + __shfl_xor(pv, 16);
+    pv = pv + __shfl_xor(pv, 32);
+    if (g == 0) {
+      const pf4 v = {p3[0], p3[1], p3[2], p3[3]};
       *(pf4*)(outs + (16 * nt + n) * 8) = v;
-      outs[(16 * nt + n) * 8 + 4] = pv[nt];
+      outs[(16 * nt + n) * 8 + 4] = pv;
     }
   }
-  wave_lds_sync();
+  wave_lds_sync();  // the outputs are written before any lane reads its walker's
   const pf4 b3 = *(const pf4*)(Wz + BA3);
   const pf4 o = *(const pf4*)(outs + wl * 8);
 #pragma unroll

@@ -82,4 +82,46 @@ def test_csharp_host_sequence_until_first_train(wk, orc):
         trained = True
         break  # later episodes sample from weights 5e-6 apart: no longer bit-comparable
     assert trained
-    assert short_episodes > 0  # the zero-loss case was exercised (the untrained walker falls fast)
+
+
+def test_csharp_host_short_episodes_append_zero_losses(wk, orc):
+    """MaxTimesteps = 30: every episode ends within 31 steps, floor(T / 64) == 0, so Train runs
+    no minibatch and ConsoleRenderer still receives valueLoss = actorLoss = 0 per episode
+    (PPOAgent.cs:153-166, ConsoleRenderer.cs:85-94): HeadlessEnvironment appends the zeros
+    without calling wk_ppo_update (which refuses an empty minibatch sequence), the weights stay
+    untouched, and the three data-collection lists stay in step"""
+    eng = wk.Engine(1, seed=SEED, Horizon=31, Minibatch=64, MinibatchGlobal=64, MaxTimesteps=30)
+    ag = orc.Agent(seed=SEED)
+    eng.set_weights(ag.params())
+    env = orc.Env(MaxTimesteps=30)
+    w0 = eng.get_weights()
+    total_rewards, critic_losses, actor_losses, best = [], [], [], 0.0
+    gstep = 0
+    for episode in range(3):
+        R = []
+        for _ in range(31):
+            out = eng.step_sampled(1)
+            a = out["actions"][0, 0]
+            oa, _ = ag.sample(out["states"][0, 0], SEED, 0, gstep)
+            gstep += 1
+            np.testing.assert_allclose(a, oa, rtol=1e-5, atol=1e-5)
+            _, r, d = env.step(a)
+            assert r == out["rewards"][0, 0] and d == out["dones"][0, 0]
+            np.testing.assert_array_equal(out["position"][0, 0], env.step_position())
+            best = max(best, float(out["position"][0, 0, 0]))  # Step's _bestDistance (:119)
+            R.append(r)
+            if d:
+                break
+        assert d and len(R) < 64
+        total_rewards.append(np.float32(np.sum(np.asarray(R, np.float64))))
+        with pytest.raises(wk.WkError, match="larger than the pool"):
+            eng.set_trajectory(*(np.zeros((len(R), 1, k), np.float32) for k in (12, 4, 4)),
+                               np.zeros((len(R), 1), np.float32), np.ones((len(R), 1), np.uint8),
+                               np.zeros((len(R), 1), np.float32))
+            eng.ppo_update(epochs=5, minibatch=64, minibatch_global=64, update_index=episode)
+        critic_losses.append(0.0)
+        actor_losses.append(0.0)
+    assert len(total_rewards) == len(critic_losses) == len(actor_losses) == 3
+    assert critic_losses == actor_losses == [0.0] * 3
+    np.testing.assert_array_equal(eng.get_weights(), w0)
+    assert best > 0.0
