@@ -264,11 +264,12 @@ def time_iterations(eng, args, k, horizon, update_index, barrier=None, physics_o
 
 
 def extra_config(wk, torch, args, n, M, M_global, horizon, physics_only=False, materials=False,
-                 k=5):
-    """one of BASELINE's other shapes on this GPU (same regime protocol as the main line)"""
+                 k=5, rough=False):
+    """one of BASELINE's other shapes on this GPU (same regime protocol as the main line);
+    rough: the same loop on CreateRoughFloor's terrain"""
     eng = wk.Engine(n, seed=args.seed, Horizon=horizon, Minibatch=M, MinibatchGlobal=M_global,
                     Epochs=args.epochs, RandomizeStart=1, RandomizeMaterial=int(materials),
-                    LanesPerWalker=args.lanes)
+                    LanesPerWalker=args.lanes, RoughFloor=int(rough))
     try:
         if physics_only:
             g = torch.Generator(device="cuda").manual_seed(args.seed)
@@ -311,6 +312,16 @@ def extra_config(wk, torch, args, n, M, M_global, horizon, physics_only=False, m
         eng.close()
 
 
+def _claim_stdout():
+    """the driver reads stdout for ONE JSON line; libraries print to fd 1 on their own (RCCL's
+    version banner at the first collective), so fd 1 goes to stderr for the whole run and the
+    JSON line is written to the original stdout"""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
 def allreduce_one_rank(wk, eng, args, horizon, update_index):
     """the collective path on one GPU -- a one-rank RCCL communicator makes
     wk_ppo_update run ordered reduction -> ncclAllReduce (24.6 KB, on the engine stream) ->
@@ -333,6 +344,7 @@ def allreduce_one_rank(wk, eng, args, horizon, update_index):
 
 def main():
     args = parse()
+    json_out = _claim_stdout()
     import wk
     from wk.dist import broadcast_unique_id, env_from_launcher, make_shard
 
@@ -503,6 +515,9 @@ def main():
         ex["config4_shard_8192"] = extra_config(wk, torch, args, 8192, 8192, 65536, T)
         ex["config5_shard_8192"] = extra_config(wk, torch, args, 8192, 8192, 65536, T,
                                                 materials=True)
+        ex["rough_floor_65536"] = extra_config(wk, torch, args, 65536, 65536, 65536, T, rough=True)
+        ex["rough_floor_shard_8192"] = extra_config(wk, torch, args, 8192, 8192, 65536, T,
+                                                    rough=True)
         out["configs"] = ex
     if cpu is not None:
         out["cpu_baseline"] = cpu
@@ -510,7 +525,7 @@ def main():
         out["rehearsal"] = ("all ranks on one GPU, host all-reduce over gloo: a check of the "
                             "multi-rank path, not a performance number")
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()

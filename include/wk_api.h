@@ -80,7 +80,7 @@ typedef struct wk_config {
   int Iterations;           /* 50 physics substeps per env-step */
   int MaxTimesteps;         /* 1000 */
   int RoughFloor;           /* 0; 1: CreateRoughFloor's 10 static segments with a per-walker
-                               Philox terrain (1- and 16-lane mappings only) */
+                               Philox terrain (every mapping) */
   int Epochs;               /* 5 */
   int BatchSize;            /* 64 */
   int UseGAE;               /* 0 */
@@ -107,8 +107,7 @@ typedef struct wk_config {
                                walker, left / right leg chains in parallel; 4 = two lanes per
                                leg (SAT axes and contact faces split; for shards of at most
                                one wave per SIMD); 16 = SAT axes over a 16-lane row; 1 = one
-                               walker per lane; 0 = auto (flat floor: 4 up to 16,384
-                               walkers, else 2; 16 with RoughFloor) */
+                               walker per lane; 0 = auto (4 up to 16,384 walkers, else 2) */
 } wk_config;
 
 /* The host-only fields of the reference's JSON configuration (SerializableHyperparameters,

@@ -238,8 +238,6 @@ static int validate(const wk_config* c, std::string& why) {
   if (c->Lambda <= 0 || c->Lambda > 1) return bad("Invalid lambda value, should be in range 0<x<1");
   if (c->Epsilon <= 0 || c->Epsilon > 1) return bad("Invalid epsilon value, should be in range 0<x<1");
   if (c->LogStandardDeviation <= -5 || c->LogStandardDeviation >= 5) return bad("Invalid log standard deviation value, should be in range -5<x<5");
-  if (c->RoughFloor && (c->LanesPerWalker == 2 || c->LanesPerWalker == 4))
-    return bad("RoughFloor runs on the 1- and 16-lane mappings (LanesPerWalker 0, 1 or 16)");
   if (c->CriticNeuralNetwork && strcmp(c->CriticNeuralNetwork, kCriticDefault) != 0) {
     snprintf(b, sizeof(b), "critic network '%s' unsupported: the kernels implement '%s'", c->CriticNeuralNetwork, kCriticDefault);
     why = b;
@@ -317,8 +315,9 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   // where the split shortens each wave's chain), 11.7 vs 7.6 ms at 32,768 (two waves per
   // SIMD: issue-bound, the split's extra selects and exchanges cost more than they save).
   // Round 1: the pair mapping 32.1 ms at 8,192 walkers vs 83.2 ms for the 16-lane rows and
-  // 104 ms one lane per walker (T = 64).  The rough floor runs on the 16-lane rows.
-  P.lanes = c.LanesPerWalker ? c.LanesPerWalker : (c.RoughFloor ? 16 : (n_env <= 16384 ? 4 : 2));
+  // 104 ms one lane per walker (T = 64).  The rough floor takes the same choice: its segment
+  // pairs run unsplit in every mapping, the leg-leg pairs keep the pair / quad split.
+  P.lanes = c.LanesPerWalker ? c.LanesPerWalker : (n_env <= 16384 ? 4 : 2);
   P.rough = c.RoughFloor ? 1 : 0;
   const float PI_F = 3.14159265358979323846f;
   x->lp_const = -logf(P.std_) - logf(sqrtf(2.0f * PI_F));

@@ -20,11 +20,11 @@
 #include "wk_kernels.h"
 #include "wk_mfma_layout.h"
 
-// Build parts (the Makefile compiles this file three times, in parallel): kernels are
+// Build parts (the Makefile compiles this file five times, in parallel): kernels are
 // templates instantiated where the host shims at the end launch them, so each part holds the
-// shims of one family -- 1: the pair / quad side kernels, 2 and 4: the scene-prop kernel
-// (given actions / policy), 3: the rest (1- and 16-lane kernels, the counting replay, init,
-// obs, policy, returns).  0: all.
+// shims of one family -- 1: the pair / quad side kernels, 5: the same on the rough floor, 2 and
+// 4: the scene-prop kernel (given actions / policy), 3: the rest (1- and 16-lane kernels, the
+// counting replay, init, obs, policy, returns).  0: all.
 #ifndef WK_PHYS_PART
 #define WK_PHYS_PART 0
 #endif
@@ -479,8 +479,8 @@ DEV void rough_segment(Poly<4>& f, int k, float yprev, float y) {
 
 // a walker part's candidate pair(s) against the floor: the flat box (Environment.cs:211-226)
 // or, with RoughFloor, the 10 static segments in list order (ter: this walker's 11 terrain
-// heights in LDS, stride 64)
-template <int N, bool TRACE, int L, bool ROUGH>
+// heights in LDS, stride TS)
+template <int N, bool TRACE, int L, bool ROUGH, int TS = 64>
 DEV void floor_pairs(Poly<N>& P, Dyn& D, const Mat& m, bool& col, PairTraceDev* tr, int pi,
                      int sub, const float* ter, uint32_t* ec = nullptr) {
   Dyn dfl;
@@ -490,7 +490,7 @@ DEV void floor_pairs(Poly<N>& P, Dyn& D, const Mat& m, bool& col, PairTraceDev* 
 #pragma unroll 1
     for (int k = 0; k < 10; k++) {
       Poly<4> seg;
-      rough_segment(seg, k, ter[k * 64], ter[(k + 1) * 64]);
+      rough_segment(seg, k, ter[k * TS], ter[(k + 1) * TS]);
       resolve_pair<N, 4, true, TRACE, L, true>(P, D, m, seg, dfl, mf, col, tr, -1, sub, nullptr, ec);
     }
   } else {
@@ -972,9 +972,12 @@ DEV void get_obs_side(const SideState& s, int side, float o[12]) {
   o[11] = left ? otup : tup;
 }
 
-template <bool TRACE, int Q>
+// ROUGH: the floor candidates are CreateRoughFloor's 10 segments (floor_pairs, general SAT /
+// contacts, replicated in both halves of the quad mapping; ter: this walker's terrain column in
+// LDS with stride TS); the leg-leg pairs keep their split
+template <bool TRACE, int Q, bool ROUGH = false, int TS = 1>
 DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
-                      PairTraceDev* tr, int side, int half, RegionProf* rp) {
+                      PairTraceDev* tr, int side, int half, RegionProf* rp, const float* ter = nullptr) {
   rp_mark(rp, RP_OTHER);
   Poly<4> fl;
   floor_poly(fl);
@@ -1002,7 +1005,10 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
 #pragma unroll
   for (int q = 0; q < 3; q++) {  // [floor if post], other segment, [floor if episode 0]
     if (q == 1) resolve_pair<6, 6, false, TRACE, 1, false, Q>(s.lo, s.dlo, mp, s.up, s.dup, mp, s.clo, tr, pb + 0, half, rp);
-    else if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1, false, Q>(s.lo, s.dlo, mp, fl, dfl, mf, s.clo, tr, pb + 1, half, rp);
+    else if ((q == 0) == s.post) {
+      if constexpr (ROUGH) floor_pairs<6, TRACE, 1, true, TS>(s.lo, s.dlo, mp, s.clo, tr, pb + 1, 0, ter);
+      else resolve_pair<6, 4, true, TRACE, 1, false, Q>(s.lo, s.dlo, mp, fl, dfl, mf, s.clo, tr, pb + 1, half, rp);
+    }
     rp_mark(rp, RP_OTHER);
   }
   integrate(s.up, s.dup, dt, adx, ady);
@@ -1010,14 +1016,18 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
 #pragma unroll
   for (int q = 0; q < 3; q++) {
     if (q == 1) resolve_pair<6, 6, false, TRACE, 1, false, Q>(s.up, s.dup, mp, s.lo, s.dlo, mp, s.cup, tr, pb + 2, half, rp);
-    else if ((q == 0) == s.post) resolve_pair<6, 4, true, TRACE, 1, false, Q>(s.up, s.dup, mp, fl, dfl, mf, s.cup, tr, pb + 3, half, rp);
+    else if ((q == 0) == s.post) {
+      if constexpr (ROUGH) floor_pairs<6, TRACE, 1, true, TS>(s.up, s.dup, mp, s.cup, tr, pb + 3, 0, ter);
+      else resolve_pair<6, 4, true, TRACE, 1, false, Q>(s.up, s.dup, mp, fl, dfl, mf, s.cup, tr, pb + 3, half, rp);
+    }
     rp_mark(rp, RP_OTHER);
   }
   // the torso's step, replicated in both lanes (traced by the left lane)
   integrate(s.body, s.dbody, dt, adx, ady);
   rp_mark(rp, RP_INTEG);
-  resolve_pair<5, 4, true, TRACE, 1>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody,
-                                     side == 0 ? tr : nullptr, 4, 0, rp);
+  if constexpr (ROUGH) floor_pairs<5, TRACE, 1, true, TS>(s.body, s.dbody, mb, s.cbody, side == 0 ? tr : nullptr, 4, 0, ter);
+  else resolve_pair<5, 4, true, TRACE, 1>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody,
+                                          side == 0 ? tr : nullptr, 4, 0, rp);
   rp_mark(rp, RP_OTHER);
 }
 
@@ -1134,6 +1144,9 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool wri
   wave_lds_sync();  // outputs read before the next env-step rewrites the tile
 }
 
+#ifndef WK_QUAD_WAVES
+#define WK_QUAD_WAVES 1  // waves per SIMD the quad mapping is built for
+#endif
 #ifndef WK_SIDE_BLOCK
 #define WK_SIDE_BLOCK 256
 #endif
@@ -1141,9 +1154,9 @@ constexpr int SIDE_BLOCK = WK_SIDE_BLOCK;  // 4 waves: the policy's weight image
 // Q = 1: a lane pair per walker (L = 2); Q = 2: a lane quad (L = 4, side = lane bit 0, half =
 // lane bit 1), for shards of at most one wave per SIMD, where the split shortens each wave's
 // dependent chain -- with room for every register (one wave per SIMD: no spills)
-template <bool POLICY, bool RECORD, bool TRACE, int Q>
+template <bool POLICY, bool RECORD, bool TRACE, int Q, bool ROUGH = false>
 __global__ __launch_bounds__(SIDE_BLOCK)
-__attribute__((amdgpu_waves_per_eu(Q == 2 ? 1 : WK_ENV_WAVES, Q == 2 ? 1 : WK_ENV_WAVES)))
+__attribute__((amdgpu_waves_per_eu(Q == 2 ? WK_QUAD_WAVES : WK_ENV_WAVES, Q == 2 ? WK_QUAD_WAVES : WK_ENV_WAVES)))
 void k_env_side(EnvParams P, StepArgs A) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int side = tid & 1;
@@ -1157,6 +1170,16 @@ void k_env_side(EnvParams P, StepArgs A) {
   const bool leader = side == 0 && half == 0 && active;
   __shared__ float pol_lds[POLICY ? (SIDE_BLOCK / 64) * 768 : 1];
   __shared__ float wz_lds[POLICY ? mf::WEND : 1];  // operand-order weights (41 KB, 2 blocks/CU)
+  // RoughFloor: the walker's terrain heights 800 + Random.Next(0, 100) (Environment.cs:242-250),
+  // [draw][walker of block]; the walker's lanes write the same values and read only its column
+  constexpr int WPB = SIDE_BLOCK >> SH;
+  __shared__ float ter_lds[ROUGH ? 11 * WPB : 1];
+  const float* const ter = ter_lds + (threadIdx.x >> SH);
+  if constexpr (ROUGH) {
+#pragma unroll 1
+    for (int i = 0; i < 11; i++)
+      ter_lds[i * WPB + (threadIdx.x >> SH)] = 800.0f + (float)terrain_draw(P.seed, (uint32_t)(P.env_offset + e), i);
+  }
   if (POLICY) {
     for (int i = threadIdx.x; i < mf::WEND / 4; i += SIDE_BLOCK)
       ((pf4*)wz_lds)[i] = ((const pf4*)A.Wz)[i];
@@ -1217,7 +1240,7 @@ void k_env_side(EnvParams P, StepArgs A) {
 #pragma unroll 1
     for (int it = 0; it < P.iterations; it++) {
       PairTraceDev* tr = (TRACE && active && half == 0) ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
-      substep_side<TRACE, Q>(s, mp, mb, dt, adx, ady, tr, side, half, rp);
+      substep_side<TRACE, Q, ROUGH, WPB>(s, mp, mb, dt, adx, ady, tr, side, half, rp, ter);
     }
     // Walker.Update + terminal flags (both upper legs and the torso)
     s.prevx = s.posx; s.prevy = s.posy;
@@ -1385,19 +1408,25 @@ static void launch_lanes(int mode, const EnvParams& P, const StepArgs& A, hipStr
   if (P.rough) launch_lanes_floor<L, true>(mode, P, A, s);
   else launch_lanes_floor<L, false>(mode, P, A, s);
 }
-#if WK_PART(1)
-template <int Q>
+#if WK_PART(1) || WK_PART(5)
+template <int Q, bool ROUGH>
 static void launch_side(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
   dim3 blk(SIDE_BLOCK), grd((unsigned)(((size_t)P.n_env * 2 * Q + SIDE_BLOCK - 1) / SIDE_BLOCK));
   switch (mode) {
-    case 0: hipLaunchKernelGGL((k_env_side<false, false, false, Q>), grd, blk, 0, s, P, A); break;
-    case 1: hipLaunchKernelGGL((k_env_side<false, false, true, Q>), grd, blk, 0, s, P, A); break;
-    case 2: hipLaunchKernelGGL((k_env_side<true, false, false, Q>), grd, blk, 0, s, P, A); break;
-    default: hipLaunchKernelGGL((k_env_side<true, true, false, Q>), grd, blk, 0, s, P, A); break;
+    case 0: hipLaunchKernelGGL((k_env_side<false, false, false, Q, ROUGH>), grd, blk, 0, s, P, A); break;
+    case 1: hipLaunchKernelGGL((k_env_side<false, false, true, Q, ROUGH>), grd, blk, 0, s, P, A); break;
+    case 2: hipLaunchKernelGGL((k_env_side<true, false, false, Q, ROUGH>), grd, blk, 0, s, P, A); break;
+    default: hipLaunchKernelGGL((k_env_side<true, true, false, Q, ROUGH>), grd, blk, 0, s, P, A); break;
   }
 }
-void launch_side_pair(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) { launch_side<1>(mode, P, A, s); }
-void launch_side_quad(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) { launch_side<2>(mode, P, A, s); }
+#endif
+#if WK_PART(1)
+void launch_side_pair(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) { launch_side<1, false>(mode, P, A, s); }
+void launch_side_quad(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) { launch_side<2, false>(mode, P, A, s); }
+#endif
+#if WK_PART(5)  // RoughFloor on the pair / quad mappings (their own build part: compile time)
+void launch_side_pair_rough(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) { launch_side<1, true>(mode, P, A, s); }
+void launch_side_quad_rough(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) { launch_side<2, true>(mode, P, A, s); }
 #endif
 #if WK_PART(2)
 void launch_env_scene_given(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
@@ -1418,6 +1447,8 @@ void launch_env_scene_policy(int mode, const EnvParams& P, const StepArgs& A, co
 #if WK_PART(3)
 void launch_side_pair(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s);
 void launch_side_quad(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s);
+void launch_side_pair_rough(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s);
+void launch_side_quad_rough(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s);
 void launch_env_scene_given(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
                             hipStream_t s);
 void launch_env_scene_policy(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
@@ -1435,8 +1466,8 @@ hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipS
     hipLaunchKernelGGL((k_env_step<false, false, false, 1, false, true>), grd, blk, 0, s, P, A);
     return hipGetLastError();
   }
-  if (P.lanes == 2) launch_side_pair(mode, P, A, s);
-  else if (P.lanes == 4) launch_side_quad(mode, P, A, s);
+  if (P.lanes == 2) (P.rough ? launch_side_pair_rough : launch_side_pair)(mode, P, A, s);
+  else if (P.lanes == 4) (P.rough ? launch_side_quad_rough : launch_side_quad)(mode, P, A, s);
   else if (P.lanes == 16) launch_lanes<16>(mode, P, A, s);
   else launch_lanes<1>(mode, P, A, s);
   return hipGetLastError();

@@ -294,19 +294,20 @@ __global__ void k_grad_reduce2(const float* __restrict__ part2, int ngroups, flo
   grad[p] = sum_groups(part2, ngroups, p);
 }
 
-// DenseLayer.Adam (DenseLayer.cs:125-159) for one parameter
-DEV void adam_param(const AdamArgs& a, int p, float gr) {
-  float m = (gr * a.c1) + (a.m[p] * a.beta1);
-  float v = (a.v[p] * a.beta2) + ((gr * gr) * a.c2);
+// DenseLayer.Adam (DenseLayer.cs:125-159) for one parameter, from its current m, v, w
+DEV void adam_apply(const AdamArgs& a, int p, float gr, float m0, float v0, float w0) {
+  float m = (gr * a.c1) + (m0 * a.beta1);
+  float v = (v0 * a.beta2) + ((gr * gr) * a.c2);
   a.m[p] = m;
   a.v[p] = v;
   float mh = m / a.bc1;
   float vh = v / a.bc2;
   float den = sqrtf(vh) + a.eps;
-  const float w = a.W[p] - ((mh / den) * a.alpha);
+  const float w = w0 - ((mh / den) * a.alpha);
   a.W[p] = w;
   if (a.Wz) mf_scatter_param(a.Wz, p, w);
 }
+DEV void adam_param(const AdamArgs& a, int p, float gr) { adam_apply(a, p, gr, a.m[p], a.v[p], a.W[p]); }
 
 // elementwise over all 6149 parameters
 __global__ void k_adam(AdamArgs a) {
@@ -341,6 +342,12 @@ __global__ __launch_bounds__(RG * QB) void k_grad_reduce_fused(const float* __re
   const int qi = threadIdx.x % QB, gi = threadIdx.x / QB;
   const int q = blockIdx.x * QB + qi;  // parameters 4q .. 4q + 3
   const int ngroups = (nblocks + RG - 1) / RG;
+  // the Adam operands do not depend on the reduction: their loads go out with the slab loads
+  // (one memory latency per minibatch tail instead of two)
+  const int pa = 4 * q + gi;
+  const bool adam_lane = ADAM && gi < 4 && pa < NPARAM;
+  float m0 = 0.0f, v0 = 0.0f, w0 = 0.0f;
+  if (adam_lane) { m0 = a.m[pa]; v0 = a.v[pa]; w0 = a.W[pa]; }
   float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (q < SLAB / 4 && gi < ngroups) {
     const int b0 = gi * RG;
@@ -364,7 +371,7 @@ __global__ __launch_bounds__(RG * QB) void k_grad_reduce_fused(const float* __re
     float t = 0.0f;
     for (int g = 0; g < ngroups; g++) t = t + gf[(g * QB + qi) * 4 + gi];
     grad[p] = t;
-    if (ADAM && p < NPARAM) adam_param(a, p, t);
+    if (adam_lane) adam_apply(a, p, t, m0, v0, w0);
   }
 }
 

@@ -2,7 +2,7 @@
 
   python scripts/phys_bench.py [n_walkers] [T] [lanes...]
 Prints ms per launch and env-steps/s for each lane mapping.  WK_SCENE=1: with the four scene
-props of tests/test_gpu_scene.py (scene_a; the one-lane scene kernel).
+props of tests/test_gpu_scene.py (scene_a; the one-lane scene kernel).  WK_ROUGH=1: RoughFloor.
 """
 import os
 import sys
@@ -17,7 +17,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 lanes = [int(x) for x in sys.argv[3:]] or [1, 2, 16]
 for L in lanes:
-    eng = wk.Engine(n, seed=20250905, Horizon=T, RandomizeStart=1, LanesPerWalker=L)
+    eng = wk.Engine(n, seed=20250905, Horizon=T, RandomizeStart=1, LanesPerWalker=L,
+                    RoughFloor=int(os.environ.get("WK_ROUGH", "0")))
     if os.environ.get("WK_SCENE"):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from test_gpu_scene import scene_a

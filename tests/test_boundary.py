@@ -86,11 +86,14 @@ def test_bad_arguments(wk):
     assert lib.wk_step(None, None, 1, None, None, None, None) == -1
 
 
-def test_rough_floor_needs_row_mappings(wk):
-    """RoughFloor runs on the 1- and 16-lane mappings; the 2-lane leg split is refused
-    (before any device is touched)"""
+def test_rough_floor_accepted_on_every_mapping(wk):
+    """RoughFloor runs on every mapping (1, 2, 4 and 16 lanes per walker, and auto): the
+    configuration is never refused (without a GPU the create fails later, at the device)"""
     lib = wk.load_library()
-    cfg = wk.default_config(RoughFloor=1, LanesPerWalker=2)
-    h = C.c_void_p()
-    assert lib.wk_create(C.byref(cfg), 0, 4, 1, C.byref(h)) == -3
-    assert b"RoughFloor" in lib.wk_last_error(None)
+    for lanes in (0, 1, 2, 4, 16):
+        cfg = wk.default_config(RoughFloor=1, LanesPerWalker=lanes)
+        h = C.c_void_p()
+        rc = lib.wk_create(C.byref(cfg), 0, 4, 1, C.byref(h))
+        if rc == 0:
+            lib.wk_destroy(h)
+        assert rc != -3, (lanes, lib.wk_last_error(None))

@@ -4,7 +4,8 @@ CreateRoughFloor (Environment.cs:230-261) builds 10 static 4-vertex Metal segmen
 the walker (15 bodies; the walker is re-appended after them on every reset).  The
 reference's unseeded Random is replaced by a per-walker Philox terrain (documented
 deviation); the oracle uses the same draws.  Bars as for the flat floor: bodies, flags,
-rewards and dones bit-exact for the 1- and 16-lane mappings."""
+rewards and dones bit-exact for every mapping (1, 2, 4 and 16 lanes per walker; the pair and
+quad mappings resolve the segment pairs unsplit and keep their leg-leg split)."""
 import numpy as np
 import pytest
 
@@ -12,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 SEED = 20250905
 F = np.float32
-lanes_param = pytest.mark.parametrize("lanes", [1, 16])
+lanes_param = pytest.mark.parametrize("lanes", [1, 2, 4, 16])
 
 
 def rough_envs(orc, n, offset=0):
@@ -90,12 +91,13 @@ def test_rough_body_views(wk, orc):
         eng.body_view(0, 15)
 
 
-def test_rough_first_segment_degenerate_edges(wk, orc):
+@pytest.mark.parametrize("lanes", [2, 4, 16])
+def test_rough_first_segment_degenerate_edges(wk, orc, lanes):
     """walkers placed over segment 0 (three collinear vertices; a zero edge when draws 0
     and 1 coincide -- about 1 walker in 100): SAT skips the zero axis and the contact
     faces take Normalize's NaN exactly as the reference does"""
     n, k = 4096, 25
-    eng = wk.Engine(n, seed=SEED, RoughFloor=1, LanesPerWalker=16)
+    eng = wk.Engine(n, seed=SEED, RoughFloor=1, LanesPerWalker=lanes)
     eng.set_offsets(np.full(n, -150.0, F))  # start x = -25
     eng.reset()
     envs = [orc.Env(dx=-150.0, rough=(SEED, e)) for e in range(n)]
