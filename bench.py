@@ -49,6 +49,7 @@ PEAK_HBM_GBS = 8000.0
 # critic (PPOAgent.cs:218-346, DenseLayer.cs:103-120); Adam ~14 flop x 6,149 per minibatch
 FLOP_GRAD_SAMPLE = 36569
 FLOP_ADAM_MINIBATCH = 86086
+GRAD_BURST = 64  # back-to-back gradient launches timed for the update roofline
 SLAB_BYTES = 6152 * 4  # gradient + 3 diagnostics, padded to 16 B: the all-reduce payload
 # SURVEY.md 8(d) flop model, priced per counted physics event (wk_count_events):
 FLOP_INTEGRATE = 477          # per walker-substep: 4 poles x 95 + hull 81 + floor 16
@@ -209,12 +210,14 @@ def valu_ceiling(lanes_per_walker, walkers):
             "(a wave64 VALU instruction per 4 cycles)")
 
 
-def update_roofline(prof_k, samples_per_minibatch, walkers, horizon, epochs, update_ms):
+def update_roofline(prof_k, samples_per_minibatch, walkers, horizon, epochs, update_ms, burst_ms):
     """SURVEY 8(d) update roofline: the gradient kernel (k_ppo_grad_ws, one launch per
-    minibatch) priced at 36,569 flop per sample over its mean HIP-event launch time, and the
-    whole update (gradient + reduction + Adam over all minibatches) over its measured time"""
+    minibatch) priced at 36,569 flop per sample over its mean duration -- HIP events around a
+    burst of back-to-back launches (wk_time_gradient): an event pair around every launch of the
+    update adds ~4 us of event overhead to a ~35 us kernel -- and the whole update (gradient +
+    reduction + Adam over all minibatches) over its measured time"""
     launches = max(1, prof_k.get("grad_launches", 0))
-    grad_us = prof_k["grad_ms"] / launches * 1e3
+    grad_us = burst_ms * 1e3
     achieved = FLOP_GRAD_SAMPLE * samples_per_minibatch / (grad_us * 1e-6) / 1e12
     n_mb = epochs * (walkers * horizon // samples_per_minibatch)
     upd_flop = epochs * walkers * horizon * FLOP_GRAD_SAMPLE + n_mb * FLOP_ADAM_MINIBATCH
@@ -223,13 +226,15 @@ def update_roofline(prof_k, samples_per_minibatch, walkers, horizon, epochs, upd
             "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
             "samples_per_launch": samples_per_minibatch, "flop_per_sample": FLOP_GRAD_SAMPLE,
-            "mean_launch_us": grad_us, "launches": launches,
+            "mean_launch_us": grad_us, "burst_launches": GRAD_BURST,
+            "mean_launch_us_per_launch_events": prof_k["grad_ms"] / launches * 1e3,
             "reduce_adam_us": prof_k["reduce_ms"] / max(1, prof_k.get("reduce_launches", 0)) * 1e3,
             "update": {"minibatches": n_mb, "flop": upd_flop, "ms": update_ms,
                        "achieved": upd_tf, "frac": upd_tf / PEAK_FP32_TFLOPS},
             "note": ("achieved = 36,569 flop/sample (SURVEY 8(d)) x samples per launch / mean "
-                     "gradient-kernel launch time (HIP events on the engine stream, one untimed "
-                     "profiled iteration)")}
+                     "gradient-kernel duration (one HIP-event pair on the engine stream around "
+                     f"{GRAD_BURST} back-to-back launches on minibatch 0 of the timed iteration's "
+                     "trajectory, after the timed region)")}
 
 
 def flops_per_env_step(ev):
@@ -300,6 +305,7 @@ def extra_config(wk, torch, args, n, M, M_global, horizon, physics_only=False, m
         eng.profile_enable(0)
         prof_k = eng.profile()
         upd_ms = prof["update_ms"] / max(1, prof["update_calls"])
+        burst = eng.time_gradient(M, GRAD_BURST)
         return {"walkers": n, "minibatch": M, "minibatch_global": M_global,
                 "env_steps_per_s": k * n * horizon / dt,
                 "rollout_ms": prof["physics_ms"] / max(1, prof["physics_launches"]),
@@ -307,7 +313,7 @@ def extra_config(wk, torch, args, n, M, M_global, horizon, physics_only=False, m
                 / max(1e-9, prof["physics_ms"] * 1e-3),
                 "ppo_update_ms": upd_ms,
                 "minibatches_per_update": args.epochs * (n * horizon // M),
-                "roofline_update": update_roofline(prof_k, M, n, horizon, args.epochs, upd_ms)}
+                "roofline_update": update_roofline(prof_k, M, n, horizon, args.epochs, upd_ms, burst)}
     finally:
         eng.close()
 
@@ -414,6 +420,8 @@ def main():
     time_iterations(eng, args, 1, T, upd)
     eng.profile_enable(0)
     prof_k = eng.profile()
+    # untimed: the gradient kernel alone, back to back (the update roofline's duration)
+    grad_burst_ms = eng.time_gradient(shard.minibatch_local, GRAD_BURST)
     # untimed: the same rollout's physics events (counting replay of its actions)
     eng.restore()
     eng.rollout(T)
@@ -503,7 +511,7 @@ def main():
         },
         "kernel_ms_one_step": {k: v for k, v in prof_k.items() if k.endswith("_ms")},
         "roofline_update": update_roofline(prof_k, shard.minibatch_local, shard.n_local, T,
-                                           args.epochs, upd_ms_max / args.steps),
+                                           args.epochs, upd_ms_max / args.steps, grad_burst_ms),
     }
     if world == 1 and not args.rehearse:
         out["allreduce_1rank"] = allreduce_one_rank(wk, eng, args, T, upd)

@@ -270,7 +270,9 @@ int wk_get_body_view(wk_ctx* ctx, int env, int body /* 0..4 walker, 5 floor (5..
 /* policy / value */
 /* Scene props for every walker (n_props <= WK_MAX_PROPS, at most WK_SCENE_MAX_VERTS vertices
  * in total; 0 removes them), each initialised as described at wk_prop.  With props the
- * env-step runs the one-lane scene kernel (LanesPerWalker 0 or 1; not with RoughFloor). */
+ * env-step runs the one-lane scene kernel (LanesPerWalker 0 or 1), on either floor: with
+ * RoughFloor the list is [walker, 10 segments, props] (after a reset [segments, props,
+ * walker]), and props resolve against every segment. */
 int wk_set_scene(wk_ctx* ctx, const wk_prop* props, int n_props);
 int wk_get_prop_view(wk_ctx* ctx, int env, int prop, wk_prop_view* out);
 int wk_get_weights(wk_ctx* ctx, float* params /* WK_NPARAM */);
@@ -407,6 +409,12 @@ int wk_count_events(wk_ctx* ctx, int k, uint64_t* counts);
  * the last rollout).  op 0 saves, op 1 restores (stream-ordered device copies, no host sync); bench.py restores one before every timed iteration so
  * each measures the same regime (the throughput no longer drifts with training). */
 int wk_snapshot(wk_ctx* ctx, int op);
+
+/* The update's gradient kernel alone: `reps` back-to-back launches on minibatch 0 (update 0,
+ * epoch 0 of the keyed sequence; minibatch 0 = config Minibatch) of the current trajectory,
+ * timed by one HIP-event pair on the context's stream -- the kernel's mean duration without
+ * per-launch event overhead (bench.py's update roofline).  Writes only scratch slabs. */
+int wk_time_gradient(wk_ctx* ctx, int minibatch, int reps, double* ms_per_launch);
 
 #ifdef __cplusplus
 }

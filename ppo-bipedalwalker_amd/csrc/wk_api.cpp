@@ -698,7 +698,6 @@ int wk_set_scene(wk_ctx* c, const wk_prop* props, int n_props) {
   DevGuard dg_(c);
   if (!c || n_props < 0 || (n_props > 0 && !props)) return WK_ERR_ARG;
   if (n_props > WK_MAX_PROPS) { SETERR(c, "at most %d scene props", (int)WK_MAX_PROPS); return WK_ERR_ARG; }
-  if (n_props > 0 && c->P.rough) { SETERR(c, "scene props run with the flat floor (RoughFloor = 0)"); return WK_ERR_CONFIG; }
   if (n_props > 0 && c->cfg.LanesPerWalker > 1) {
     SETERR(c, "scene props run on the one-lane mapping (LanesPerWalker 0 or 1)");
     return WK_ERR_CONFIG;
@@ -1047,6 +1046,55 @@ static wk::GradArgs grad_base(wk_ctx* c) {
 }
 
 static int ppo_update_impl(wk_ctx* c, const wk_ppo_args* args);
+// The gradient kernel alone, `reps` back-to-back launches on minibatch 0 of the keyed sequence
+// (update 0, epoch 0) of the current trajectory, between one HIP-event pair on the context's
+// stream: the kernel's mean duration without per-launch event overhead (bench.py's update
+// roofline; the launches write only the scratch slabs, no weights change)
+int wk_time_gradient(wk_ctx* c, int minibatch, int reps, double* ms_per_launch) {
+  DevGuard dg_(c);
+  if (!c || reps <= 0 || !ms_per_launch) return WK_ERR_ARG;
+  if (c->T_valid <= 0) { SETERR(c, "wk_time_gradient before wk_rollout / wk_set_trajectory"); return WK_ERR_STATE; }
+  if (!c->returns_valid) {
+    int r = returns_impl(c);
+    if (r) return r;
+  }
+  const int M = minibatch > 0 ? minibatch : c->cfg.Minibatch;
+  const uint32_t pool = (uint32_t)((size_t)c->n * c->T_valid);
+  if ((uint32_t)M > pool) { SETERR(c, "minibatch %d larger than the pool %u", M, pool); return WK_ERR_ARG; }
+  wk::GradArgs g = grad_base(c);
+  g.states = c->ts; g.actions = c->ta; g.logp_old = c->tlp; g.returns = c->tret; g.adv = c->tadv;
+  g.pool = pool;
+  g.use_perm = 1;
+  g.samples = M;
+  g.b_div = (float)(c->cfg.MinibatchGlobal > 0 ? c->cfg.MinibatchGlobal : M);
+  g.pk = wk::perm_key(c->seed, 0u, 0u, pool);
+  g.base = 0;
+  const int nblocks = wk::ppo_grad_mfma_blocks(M);
+  const size_t need = ((size_t)nblocks + wk::grad_reduce_groups(nblocks)) * wk::SLAB;
+  if (c->partial_floats < need) {
+    if (c->partial) (void)hipFree(c->partial);
+    c->partial = nullptr;
+    c->partial_floats = 0;
+    HIPCHK(c, hipMalloc((void**)&c->partial, sizeof(float) * need));
+    c->partial_floats = need;
+  }
+  g.partial = c->partial;
+  hipEvent_t a = nullptr, b = nullptr;
+  HIPCHK(c, hipEventCreate(&a));
+  HIPCHK(c, hipEventCreate(&b));
+  HIPCHK(c, wk::launch_ppo_grad_mfma(g, nblocks, c->stream));  // warm
+  HIPCHK(c, hipEventRecord(a, c->stream));
+  for (int i = 0; i < reps; i++) HIPCHK(c, wk::launch_ppo_grad_mfma(g, nblocks, c->stream));
+  HIPCHK(c, hipEventRecord(b, c->stream));
+  HIPCHK(c, hipEventSynchronize(b));
+  float ms = 0.0f;
+  HIPCHK(c, hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  *ms_per_launch = (double)ms / reps;
+  return WK_OK;
+}
+
 int wk_ppo_update(wk_ctx* c, const wk_ppo_args* args, float* critic_diag, float* actor_diag) {
   DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
@@ -1574,9 +1622,9 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
            c->cfg.Iterations, c->cfg.MaxTimesteps, c->cfg.RoughFloor);
     return WK_ERR_CONFIG;
   }
-  if (np > 0 && (c->P.rough || c->cfg.LanesPerWalker > 1)) {  // wk_set_scene would refuse it
-    SETERR(c, "checkpoint '%s' has scene props, which need the flat floor and the one-lane "
-              "mapping (LanesPerWalker 0 or 1)", path);
+  if (np > 0 && c->cfg.LanesPerWalker > 1) {  // wk_set_scene would refuse it
+    SETERR(c, "checkpoint '%s' has scene props, which need the one-lane mapping "
+              "(LanesPerWalker 0 or 1)", path);
     return WK_ERR_CONFIG;
   }
   // the scene first: wk_set_scene is all-or-nothing and is the last step that can fail on

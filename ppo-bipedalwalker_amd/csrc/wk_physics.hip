@@ -20,11 +20,11 @@
 #include "wk_kernels.h"
 #include "wk_mfma_layout.h"
 
-// Build parts (the Makefile compiles this file five times, in parallel): kernels are
+// Build parts (the Makefile compiles this file seven times, in parallel): kernels are
 // templates instantiated where the host shims at the end launch them, so each part holds the
 // shims of one family -- 1: the pair / quad side kernels, 5: the same on the rough floor, 2 and
-// 4: the scene-prop kernel (given actions / policy), 3: the rest (1- and 16-lane kernels, the
-// counting replay, init, obs, policy, returns).  0: all.
+// 4: the scene-prop kernel (given actions / policy), 6 and 7: the same on the rough floor, 3: the
+// rest (1- and 16-lane kernels, the counting replay, init, obs, policy, returns).  0: all.
 #ifndef WK_PHYS_PART
 #define WK_PHYS_PART 0
 #endif
@@ -1385,7 +1385,7 @@ __global__ void k_returns(int n, int T, int use_gae, float gamma, float lambda,
 #endif  // WK_PART(3)
 }  // namespace wk
 
-#if WK_PART(2) || WK_PART(4)
+#if WK_PART(2) || WK_PART(4) || WK_PART(6) || WK_PART(7)
 namespace wk {
 #include "wk_scene.inc"
 }  // namespace wk
@@ -1428,21 +1428,37 @@ void launch_side_quad(int mode, const EnvParams& P, const StepArgs& A, hipStream
 void launch_side_pair_rough(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) { launch_side<1, true>(mode, P, A, s); }
 void launch_side_quad_rough(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) { launch_side<2, true>(mode, P, A, s); }
 #endif
+#if WK_PART(2) || WK_PART(6)
+template <bool ROUGH>
+static void scene_given(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S, hipStream_t s) {
+  dim3 blk(64), grd((unsigned)((P.n_env + 63) / 64));
+  if (mode == 0) hipLaunchKernelGGL((k_env_scene<false, false, false, ROUGH>), grd, blk, 0, s, P, A, S);
+  else hipLaunchKernelGGL((k_env_scene<false, false, true, ROUGH>), grd, blk, 0, s, P, A, S);
+}
+#endif
+#if WK_PART(4) || WK_PART(7)
+template <bool ROUGH>
+static void scene_policy(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S, hipStream_t s) {
+  dim3 blk(64), grd((unsigned)((P.n_env + 63) / 64));
+  if (mode == 2) hipLaunchKernelGGL((k_env_scene<true, false, false, ROUGH>), grd, blk, 0, s, P, A, S);
+  else hipLaunchKernelGGL((k_env_scene<true, true, false, ROUGH>), grd, blk, 0, s, P, A, S);
+}
+#endif
 #if WK_PART(2)
 void launch_env_scene_given(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
-                            hipStream_t s) {
-  dim3 blk(64), grd((unsigned)((P.n_env + 63) / 64));
-  if (mode == 0) hipLaunchKernelGGL((k_env_scene<false, false, false>), grd, blk, 0, s, P, A, S);
-  else hipLaunchKernelGGL((k_env_scene<false, false, true>), grd, blk, 0, s, P, A, S);
-}
+                            hipStream_t s) { scene_given<false>(mode, P, A, S, s); }
+#endif
+#if WK_PART(6)  // scene props on the rough floor (own build parts: compile time)
+void launch_env_scene_given_rough(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
+                                  hipStream_t s) { scene_given<true>(mode, P, A, S, s); }
 #endif
 #if WK_PART(4)
 void launch_env_scene_policy(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
-                             hipStream_t s) {
-  dim3 blk(64), grd((unsigned)((P.n_env + 63) / 64));
-  if (mode == 2) hipLaunchKernelGGL((k_env_scene<true, false, false>), grd, blk, 0, s, P, A, S);
-  else hipLaunchKernelGGL((k_env_scene<true, true, false>), grd, blk, 0, s, P, A, S);
-}
+                             hipStream_t s) { scene_policy<false>(mode, P, A, S, s); }
+#endif
+#if WK_PART(7)
+void launch_env_scene_policy_rough(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
+                                   hipStream_t s) { scene_policy<true>(mode, P, A, S, s); }
 #endif
 #if WK_PART(3)
 void launch_side_pair(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s);
@@ -1453,10 +1469,14 @@ void launch_env_scene_given(int mode, const EnvParams& P, const StepArgs& A, con
                             hipStream_t s);
 void launch_env_scene_policy(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
                              hipStream_t s);
+void launch_env_scene_given_rough(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
+                                  hipStream_t s);
+void launch_env_scene_policy_rough(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
+                                   hipStream_t s);
 hipError_t launch_env_scene(int mode, const EnvParams& P, const StepArgs& A, const SceneDev& S,
                             hipStream_t s) {
-  if (mode <= 1) launch_env_scene_given(mode, P, A, S, s);
-  else launch_env_scene_policy(mode, P, A, S, s);
+  if (mode <= 1) (P.rough ? launch_env_scene_given_rough : launch_env_scene_given)(mode, P, A, S, s);
+  else (P.rough ? launch_env_scene_policy_rough : launch_env_scene_policy)(mode, P, A, S, s);
   return hipGetLastError();
 }
 hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {

@@ -39,7 +39,7 @@ EXPORTS = [
     "wk_config_save_json", "wk_config_load_json", "wk_collect_data", "wk_episode_log_count",
     "wk_episode_log_drain", "wk_loss_log_drain", "wk_write_data_file",
     "wk_comm_unique_id", "wk_comm_init", "wk_comm_init_host", "wk_allreduce_test", "wk_profile_enable",
-    "wk_profile_get", "wk_profile_reset", "wk_count_events", "wk_snapshot",
+    "wk_profile_get", "wk_profile_reset", "wk_count_events", "wk_snapshot", "wk_time_gradient",
 ]
 
 
@@ -232,6 +232,7 @@ def load_library(path=None):
         "wk_comm_init": (I, [P, I, I, P]),
         "wk_allreduce_test": (I, [P, P, I]),
         "wk_comm_init_host": (I, [P, I, I, HOST_ALLREDUCE_FN, P]),
+        "wk_time_gradient": (I, [P, I, I, C.POINTER(C.c_double)]),
         "wk_profile_enable": (I, [P, I]),
         "wk_profile_get": (I, [P, C.POINTER(Profile)]),
         "wk_profile_reset": (I, [P]),
@@ -673,6 +674,14 @@ class Engine:
         x = _f32(x).copy()
         self._chk(self.lib.wk_allreduce_test(self.h, _ptr(x), x.size), "wk_allreduce_test")
         return x
+
+    def time_gradient(self, minibatch=0, reps=64):
+        """wk_time_gradient: mean ms of the update's gradient kernel over `reps` back-to-back
+        launches on minibatch 0 of the current trajectory"""
+        ms = C.c_double()
+        self._chk(self.lib.wk_time_gradient(self.h, int(minibatch), int(reps), C.byref(ms)),
+                  "wk_time_gradient")
+        return ms.value
 
     # -- counting replay / snapshots --
     def count_events(self, k):

@@ -4,7 +4,7 @@
 # and one SQ pass (instruction mix, lane utilisation).
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-R=${ROUND:-r02}
+R=${ROUND:-r03}
 OUT=gpurun_out/prof_$R
 mkdir -p $OUT
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py > $OUT/bench_trace.log 2>&1

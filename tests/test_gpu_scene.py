@@ -6,7 +6,8 @@ maintainer adds after CreateFloor() in the Environment constructor, Environment.
 and walker resets keep them (Walker.Reset only re-appends the walker's five bodies,
 Walker.cs:212-234).  The props meet the walker's parts, the floor and each other through the
 reference's ResolveCollisions (RigidBody.cs:66-113).  Bars as for the walker itself: every
-walker body, every prop vertex / velocity, rewards and dones bit-exact."""
+walker body, every prop vertex / velocity, rewards and dones bit-exact -- on the flat floor and
+on the rough floor's segments."""
 import numpy as np
 import pytest
 
@@ -34,9 +35,10 @@ def scene_b(m):  # 24 + 4 + 3 = 31 vertices: the hexagon smoothed twice
             m(shape="Triangle", material="Ice", cx=230, cy=700, size=20, ay=980)]
 
 
-def oracle_envs(orc, n, props, offset=0):
+def oracle_envs(orc, n, props, offset=0, rough=False):
     return [orc.Env(dx=float(orc.env_offset(SEED, offset + e)),
-                    material=int(orc.env_material(SEED, offset + e)), props=props)
+                    material=int(orc.env_material(SEED, offset + e)), props=props,
+                    rough=(SEED, offset + e) if rough else None)
             for e in range(n)]
 
 
@@ -157,9 +159,6 @@ def test_scene_validation(wk):
         eng.set_scene([m(size=0.0)])
     with pytest.raises(wk.WkError):
         eng.set_scene([m(material=9)])
-    rough = wk.Engine(8, seed=SEED, RoughFloor=1)
-    with pytest.raises(wk.WkError):
-        rough.set_scene([m()])
     side = wk.Engine(8, seed=SEED, LanesPerWalker=2)
     with pytest.raises(wk.WkError):
         side.set_scene([m()])
@@ -185,3 +184,57 @@ def test_scene_at_bench_scale(wk, orc):
         for p in range(4):
             np.testing.assert_array_equal(eng.prop_view(i, p).vertex_array(), e.prop(p)[0])
     assert not fault.any()
+
+
+@pytest.mark.parametrize("scene", [scene_a, scene_b])
+def test_scene_on_rough_floor_bitexact(wk, orc, scene):
+    """scene props on CreateRoughFloor's terrain (the combination the reference's
+    list-based environment admits, Environment.cs:39-51,230-261): list [walker, 10 segments,
+    props], after a reset [segments, props, walker]; every prop resolves against every
+    segment.  Bodies, props, rewards and dones bit-exact over env-steps with resets, then a
+    policy rollout replayed through the oracle"""
+    n, k, T = 128, 120, 32
+    eng = wk.Engine(n, seed=SEED, RandomizeStart=1, RandomizeMaterial=1, RoughFloor=1, Horizon=T)
+    eng.set_scene(scene(wk.make_prop))
+    envs = oracle_envs(orc, n, scene(orc.make_prop), rough=True)
+    n_props = len(scene(orc.make_prop))
+    check_props(eng, envs, n_props)
+    acts = np.random.default_rng(13).uniform(-1.2, 1.2, (k, n, 4)).astype(F)
+    obs, rew, done, fault = eng.step(acts, k=k)
+    ndone = 0
+    for i, e in enumerate(envs):
+        for t in range(k):
+            o, r, d = e.step(acts[t, i])
+            assert r == rew[t, i] and d == done[t, i], (i, t)
+            np.testing.assert_array_equal(o, obs[t, i])
+            ndone += d
+    np.testing.assert_array_equal(eng.get_state(), np.stack([e.dump() for e in envs]))
+    check_props(eng, envs, n_props)
+    assert ndone > 0 and not fault.any()
+    eng.rollout(T)
+    tr = eng.get_trajectory(T)
+    for i, e in enumerate(envs):
+        for t in range(T):
+            np.testing.assert_array_equal(tr["states"][t, i], e.obs(), err_msg=f"env {i} t {t}")
+            _, r, d = e.step(tr["actions"][t, i])
+            assert r == tr["rewards"][t, i] and d == tr["dones"][t, i], (i, t)
+    np.testing.assert_array_equal(eng.get_state(), np.stack([e.dump() for e in envs]))
+    check_props(eng, envs, n_props)
+
+
+def test_scene_on_rough_floor_trace(wk, orc):
+    """the walker's traced pairs (joints, leg-leg; segment pairs are not traced) with props on
+    the rough floor"""
+    n = 64
+    eng = wk.Engine(n, seed=SEED, RandomizeStart=1, RoughFloor=1)
+    eng.set_scene(scene_b(wk.make_prop))
+    envs = [orc.Env(dx=float(orc.env_offset(SEED, e)), props=scene_b(orc.make_prop),
+                    rough=(SEED, e)) for e in range(n)]
+    acts = np.random.default_rng(3).uniform(-1, 1, (n, 4)).astype(F)
+    tr = eng.step_traced(acts)
+    for i, e in enumerate(envs):
+        _, _, _, t = e.step(acts[i], trace=True)
+        for key in ("aabb_hit", "sat_hit", "n_contacts", "normal", "depth", "contact", "impulse",
+                    "joint_depth", "joint_impulse"):
+            np.testing.assert_array_equal(tr[i][key], t[key], err_msg=f"env {i} {key}")
+    check_props(eng, envs, 3)
