@@ -381,6 +381,16 @@ int wk_allreduce_test(wk_ctx* ctx, float* host_buf, int n); /* sum in place (tes
  * whole job -- abort every rank. */
 typedef int (*wk_host_allreduce_fn)(float* buf, int n, void* user);
 int wk_comm_init_host(wk_ctx* ctx, int rank, int nranks, wk_host_allreduce_fn fn, void* user);
+/* The one-shot exchange over peer-mapped memory instead of RCCL (ranks on one node, at most 8):
+ * wk_comm_ipc_handle allocates this rank's exchange region and returns its IPC handle; the
+ * caller all-gathers the handles (any control plane) and passes all of them, in rank order, to
+ * wk_comm_init_ipc, which maps the peers' regions.  Per minibatch one kernel publishes this
+ * rank's ordered block sum, waits (bounded, ~1 s) for every peer's, sums the ranks' slabs in
+ * rank order and applies Adam -- no collective library, no host round trip.  A peer that never
+ * publishes fails wk_ppo_update with WK_ERR_COMM (fatal for the job, as a failed all-reduce). */
+enum { WK_IPC_HANDLE_BYTES = 64 };
+int wk_comm_ipc_handle(wk_ctx* ctx, uint8_t* handle /* WK_IPC_HANDLE_BYTES */);
+int wk_comm_init_ipc(wk_ctx* ctx, int rank, int nranks, const uint8_t* handles /* nranks * 64 */);
 
 /* profiling */
 /* level 0 off; 1: HIP events around each rollout / returns pass / whole PPO update (cheap

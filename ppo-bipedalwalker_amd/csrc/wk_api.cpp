@@ -87,6 +87,13 @@ struct wk_ctx {
   wk_host_allreduce_fn host_ar = nullptr;  // wk_comm_init_host: a caller-supplied all-reduce
   void* host_ar_user = nullptr;
   std::vector<float> host_ar_buf;
+  // wk_comm_init_ipc: the one-shot exchange over peer-mapped memory (k_xch_adam)
+  void* xch = nullptr;                 // this rank's exchange region (exported by IPC handle)
+  std::vector<void*> xch_peers;        // peers' regions, opened from their handles
+  wk::XchArgs xa{};                    // slab / flag pointers of every rank
+  bool ipc = false;
+  uint64_t xch_seq = 0;
+  uint32_t* xch_err = nullptr;         // device word: a peer never published
   // profiling
   int prof = 0;  // profile level
   struct Ev { int kind; hipEvent_t a, b; int64_t units; };
@@ -394,6 +401,10 @@ int wk_destroy(wk_ctx* c) {
   for (auto& e : c->pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto e : c->pool) (void)hipEventDestroy(e);
   if (c->comm) ncclCommDestroy(c->comm);
+  for (void* p : c->xch_peers)
+    if (p) (void)hipIpcCloseMemHandle(p);
+  if (c->xch) (void)hipFree(c->xch);
+  if (c->xch_err) (void)hipFree(c->xch_err);
   void* bufs[] = {c->st, c->dxoff, c->mat, c->rng_t, c->W, c->Wz, c->m, c->v, c->grad, c->ts, c->ta,
                   c->tlp, c->tr, c->tv, c->tret, c->tadv, c->td, c->partial, c->scratch, c->scratch2,
                   c->ep_acc, c->ep_len, c->ep_scratch, c->ep_rowcnt, c->ep_count, c->ep_log,
@@ -997,7 +1008,7 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   float* part2 = c->partial + (size_t)nblocks * wk::SLAB;
   // with a communicator (any size, also one rank) the collective path runs: reduction,
   // RCCL all-reduce, Adam -- a single-GPU test then covers the multi-GPU sequence
-  const bool multi = c->comm != nullptr || c->host_ar != nullptr;
+  const bool multi = c->comm != nullptr || c->host_ar != nullptr || c->ipc;
   if (apply_adam && !multi) {  // one GPU: the last reduction stage applies Adam
     ProfScope ps(c, PK_REDUCE, 0, 2);
     HIPCHK(c, wk::launch_grad_reduce_adam(c->partial, nblocks, part2, c->grad, a, c->stream));
@@ -1006,6 +1017,18 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   {
     ProfScope ps(c, PK_REDUCE, 0, 2);
     HIPCHK(c, wk::launch_grad_reduce(c->partial, nblocks, part2, c->grad, c->stream));
+  }
+  if (c->ipc) {  // the exchange and Adam in one launch (k_xch_adam)
+    ProfScope ps(c, PK_ALLRED, 0, 2);
+    wk::XchArgs x = c->xa;
+    x.grad = c->grad;
+    x.grad_out = c->grad;
+    x.seq = ++c->xch_seq;
+    x.err = c->xch_err;
+    x.a = a;
+    if (!apply_adam) { SETERR(c, "the IPC exchange always applies Adam"); return WK_ERR_STATE; }
+    HIPCHK(c, wk::launch_xch_adam(x, c->stream));
+    return WK_OK;
   }
   if (multi) {
     ProfScope ps(c, PK_ALLRED, 0, 2);
@@ -1103,6 +1126,12 @@ int wk_ppo_update(wk_ctx* c, const wk_ppo_args* args, float* critic_diag, float*
     ProfScope ps(c, PK_UPDATE);
     int r = ppo_update_impl(c, args);
     if (r) return r;
+  }
+  if (c->ipc) {  // a peer that never published is fatal for the job (like a failed all-reduce)
+    uint32_t err = 0;
+    HIPCHK(c, hipMemcpyAsync(&err, c->xch_err, sizeof err, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (err) { SETERR(c, "IPC gradient exchange: a peer did not publish its minibatch slab"); return WK_ERR_COMM; }
   }
   if (c->collect) {  // the last minibatch's losses, as PPOAgent.Train hands them on (:165-166)
     if (c->loss_count < c->loss_cap)
@@ -1234,6 +1263,57 @@ int wk_comm_init_host(wk_ctx* c, int rank, int nranks, wk_host_allreduce_fn fn, 
   if (c->comm) { SETERR(c, "the context already has an RCCL communicator"); return WK_ERR_STATE; }
   c->host_ar = fn;
   c->host_ar_user = user;
+  c->rank = rank;
+  c->nranks = nranks;
+  return WK_OK;
+}
+
+int wk_comm_ipc_handle(wk_ctx* c, uint8_t* handle) {
+  DevGuard dg_(c);
+  if (!c || !handle) return WK_ERR_ARG;
+  static_assert(sizeof(hipIpcMemHandle_t) == WK_IPC_HANDLE_BYTES, "IPC handle size");
+  if (!c->xch) {
+    HIPCHK(c, hipMalloc(&c->xch, wk::xch_region_bytes()));
+    HIPCHK(c, hipMemset(c->xch, 0, wk::xch_region_bytes()));
+    HIPCHK(c, hipMalloc((void**)&c->xch_err, sizeof(uint32_t)));
+    HIPCHK(c, hipMemset(c->xch_err, 0, sizeof(uint32_t)));
+  }
+  hipIpcMemHandle_t h;
+  HIPCHK(c, hipIpcGetMemHandle(&h, c->xch));
+  memcpy(handle, &h, sizeof h);
+  return WK_OK;
+}
+
+int wk_comm_init_ipc(wk_ctx* c, int rank, int nranks, const uint8_t* handles) {
+  DevGuard dg_(c);
+  if (!c || !handles || nranks <= 0 || rank < 0 || rank >= nranks) return WK_ERR_ARG;
+  if (nranks > wk::XCH_MAX_RANKS) { SETERR(c, "the IPC exchange spans at most %d ranks", (int)wk::XCH_MAX_RANKS); return WK_ERR_ARG; }
+  if (c->comm || c->host_ar || c->ipc) { SETERR(c, "the context already has an all-reduce"); return WK_ERR_STATE; }
+  if (!c->xch) { SETERR(c, "wk_comm_ipc_handle first"); return WK_ERR_STATE; }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  wk::XchArgs x{};
+  std::vector<void*> opened;
+  for (int r = 0; r < nranks; r++) {
+    void* base = c->xch;
+    if (r != rank) {
+      hipIpcMemHandle_t h;
+      memcpy(&h, handles + (size_t)r * WK_IPC_HANDLE_BYTES, sizeof h);
+      const hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+      if (e != hipSuccess) {
+        for (void* p : opened) (void)hipIpcCloseMemHandle(p);
+        SETERR(c, "hipIpcOpenMemHandle (rank %d): %s", r, hipGetErrorString(e));
+        return WK_ERR_COMM;
+      }
+      opened.push_back(base);
+    }
+    x.slab[r] = (float*)base;
+    x.flag[r] = (uint64_t*)((char*)base + sizeof(float) * 2 * wk::SLAB);
+  }
+  x.rank = rank;
+  x.nranks = nranks;
+  c->xa = x;
+  c->xch_peers = opened;
+  c->ipc = true;
   c->rank = rank;
   c->nranks = nranks;
   return WK_OK;

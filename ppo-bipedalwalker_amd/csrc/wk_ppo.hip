@@ -483,6 +483,51 @@ hipError_t launch_grad_reduce_adam(const float* partial, int nblocks, float* par
                      grad, a);
   return hipGetLastError();
 }
+// One-shot exchange + Adam (wk_comm_init_ipc): the minibatch's gradient all-reduce without a
+// collective library.  Each rank publishes its ordered block sum into its own exchange region
+// (slab buffer seq & 1), releases a per-block sequence flag at system scope, waits (bounded)
+// until every peer's flag for the block reaches seq, and reads the peers' slabs directly
+// through the IPC mappings -- summing in rank order, rank 0's value first, which for two ranks
+// is the RCCL / host all-reduce's a + b bit for bit -- then applies Adam to its span of the
+// parameters.  Reuse of a buffer two minibatches later is safe: a rank publishes seq + 2 only
+// after its exchange of seq + 1 saw every peer's seq + 1 flag, which a peer sets only once
+// its own exchange of seq (the last read of the seq buffers) has completed (stream order).
+__global__ __launch_bounds__(256) void k_xch_adam(XchArgs x) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int lo = b * XCH_SPAN, hi = lo + XCH_SPAN < SLAB ? lo + XCH_SPAN : SLAB;
+  const int buf = (int)(x.seq & 1u);
+  float* const own = x.slab[x.rank] + (size_t)buf * SLAB;
+  for (int p = lo + t; p < hi; p += 256) own[p] = x.grad[p];
+  __syncthreads();  // (workgroup release: every wave's stores have reached the L2)
+  if (t == 0)
+    __hip_atomic_store(x.flag[x.rank] + b, x.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t < x.nranks && t != x.rank) {
+    uint64_t* f = x.flag[t] + b;
+    uint32_t spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < x.seq) {
+      if (++spins > (1u << 24)) {  // ~1 s: a peer is gone -- report, never hang the GPU
+        atomicOr(x.err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale peer lines
+  for (int p = lo + t; p < hi; p += 256) {
+    float acc = x.rank == 0 ? x.grad[p] : x.slab[0][(size_t)buf * SLAB + p];
+    for (int r = 1; r < x.nranks; r++)
+      acc = acc + (r == x.rank ? x.grad[p] : x.slab[r][(size_t)buf * SLAB + p]);
+    x.grad_out[p] = acc;
+    if (p < NPARAM) adam_param(x.a, p, acc);
+  }
+}
+size_t xch_region_bytes() { return sizeof(float) * 2 * SLAB + sizeof(uint64_t) * XCH_BLOCKS; }
+hipError_t launch_xch_adam(const XchArgs& x, hipStream_t s) {
+  hipLaunchKernelGGL(k_xch_adam, dim3(XCH_BLOCKS), dim3(256), 0, s, x);
+  return hipGetLastError();
+}
+
 hipError_t launch_adam(const AdamArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_adam, dim3((NPARAM + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();
