@@ -94,6 +94,10 @@ def parse():
                    help="multi-rank rehearsal on ONE GPU: every rank on device 0, gradients "
                         "all-reduced on the host over gloo (wk_comm_init_host) instead of RCCL "
                         "-- exercises the N > 1 code path; not a performance number")
+    p.add_argument("--exchange", choices=("rccl", "ipc"), default="ipc",
+                   help="N > 1 minibatch gradient exchange: the one-shot exchange over IPC-mapped "
+                        "peer memory fused with the ordered reduction and Adam (wk_comm_init_ipc; "
+                        "falls back to RCCL if the mapping fails), or the RCCL all-reduce")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_physics.json"))
     return p.parse_args()
 
@@ -386,12 +390,33 @@ def main():
                     Minibatch=shard.minibatch_local, MinibatchGlobal=shard.minibatch_global,
                     Epochs=args.epochs, EnvOffset=shard.env_offset, RandomizeStart=1,
                     RandomizeMaterial=1 if args.materials else 0, LanesPerWalker=args.lanes)
-    if world > 1 and args.rehearse:
+    exchange = args.exchange if world > 1 else "none"
+    if world > 1 and args.exchange == "ipc":
+        def allgather(b):
+            out = [None] * world
+            dist.all_gather_object(out, b)
+            return out
+        try:
+            eng.comm_init_ipc(rank, world, allgather)
+            ok = 1
+        except wk.WkError as ex:  # e.g. no peer access between the devices
+            print(f"rank {rank}: IPC exchange unavailable ({ex}); using RCCL", file=sys.stderr)
+            ok = 0
+        okt = torch.tensor([ok])
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)  # every rank takes the same exchange
+        if not okt.item():
+            eng.close()
+            eng = wk.Engine(shard.n_local, seed=args.seed, device=local, Horizon=T,
+                            Minibatch=shard.minibatch_local, MinibatchGlobal=shard.minibatch_global,
+                            Epochs=args.epochs, EnvOffset=shard.env_offset, RandomizeStart=1,
+                            RandomizeMaterial=1 if args.materials else 0, LanesPerWalker=args.lanes)
+            exchange = "host (gloo)" if args.rehearse else "rccl"
+    if world > 1 and exchange != "ipc" and args.rehearse:
         def host_allreduce(buf):
             t = torch.from_numpy(buf)
             dist.all_reduce(t)  # in place on the numpy view (gloo)
         eng.comm_init_host(rank, world, host_allreduce)
-    elif world > 1:
+    elif world > 1 and exchange != "ipc":
         uid = wk.Engine.comm_unique_id() if rank == 0 else None
         uid = broadcast_unique_id(uid)
         eng.comm_init(rank, world, uid)
@@ -480,6 +505,8 @@ def main():
             "epochs": args.epochs,
             "minibatch_global": shard.minibatch_global,
             "parallelism": f"dp{world}",
+            "exchange": (exchange if exchange in ("none", "ipc")
+                         else "host (gloo)" if args.rehearse else "rccl"),
         },
         "ppo_update_ms": upd_ms_max / args.steps,
         "rollout_env_steps_per_s": world * shard.n_local * T * args.steps / (phys_ms_max * 1e-3),

@@ -204,6 +204,8 @@ public static class Wk
     [DllImport(Lib)] public static extern int wk_comm_unique_id(byte[] id);
     [DllImport(Lib)] public static extern int wk_comm_init(IntPtr ctx, int rank, int nRanks, byte[] uniqueId);
     [DllImport(Lib)] public static extern int wk_allreduce_test(IntPtr ctx, float[] buf, int n);
+    [DllImport(Lib)] public static extern int wk_comm_ipc_handle(IntPtr ctx, byte[] handle);
+    [DllImport(Lib)] public static extern int wk_comm_init_ipc(IntPtr ctx, int rank, int nRanks, byte[] handles);
     [UnmanagedFunctionPointer(CallingConvention.Cdecl)] public delegate int HostAllReduce(IntPtr buf, int n, IntPtr user);
     [DllImport(Lib)] public static extern int wk_comm_init_host(IntPtr ctx, int rank, int nRanks, HostAllReduce fn, IntPtr user);
 

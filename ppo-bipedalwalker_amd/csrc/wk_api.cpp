@@ -1009,6 +1009,18 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   // with a communicator (any size, also one rank) the collective path runs: reduction,
   // RCCL all-reduce, Adam -- a single-GPU test then covers the multi-GPU sequence
   const bool multi = c->comm != nullptr || c->host_ar != nullptr || c->ipc;
+  if (c->ipc && apply_adam) {  // reduction, exchange and Adam in one launch (k_reduce_xch_adam)
+    ProfScope ps(c, PK_ALLRED, 0, 2);
+    wk::XchArgs x = c->xa;
+    x.partial = c->partial;
+    x.nblocks = nblocks;
+    x.grad_out = c->grad;
+    x.seq = ++c->xch_seq;
+    x.err = c->xch_err;
+    x.a = a;
+    HIPCHK(c, wk::launch_reduce_xch_adam(x, c->stream));
+    return WK_OK;
+  }
   if (apply_adam && !multi) {  // one GPU: the last reduction stage applies Adam
     ProfScope ps(c, PK_REDUCE, 0, 2);
     HIPCHK(c, wk::launch_grad_reduce_adam(c->partial, nblocks, part2, c->grad, a, c->stream));
@@ -1018,19 +1030,8 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
     ProfScope ps(c, PK_REDUCE, 0, 2);
     HIPCHK(c, wk::launch_grad_reduce(c->partial, nblocks, part2, c->grad, c->stream));
   }
-  if (c->ipc) {  // the exchange and Adam in one launch (k_xch_adam)
-    ProfScope ps(c, PK_ALLRED, 0, 2);
-    wk::XchArgs x = c->xa;
-    x.grad = c->grad;
-    x.grad_out = c->grad;
-    x.seq = ++c->xch_seq;
-    x.err = c->xch_err;
-    x.a = a;
-    if (!apply_adam) { SETERR(c, "the IPC exchange always applies Adam"); return WK_ERR_STATE; }
-    HIPCHK(c, wk::launch_xch_adam(x, c->stream));
-    return WK_OK;
-  }
-  if (multi) {
+
+  if (multi && !c->ipc) {  // (a gradient-only call on an IPC context keeps the local sum)
     ProfScope ps(c, PK_ALLRED, 0, 2);
     if (c->comm) {
       ncclResult_t r = ncclAllReduce(c->grad, c->grad, wk::SLAB, ncclFloat, ncclSum,

@@ -132,12 +132,14 @@ hipError_t launch_grad_reduce_adam(const float* partial, int nblocks, float* par
                                    const AdamArgs& a, hipStream_t s);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t s);
 
-// One-shot gradient exchange over peer-mapped (IPC) memory, fused with Adam (wk_comm_init_ipc):
-// rank r's exchange region is [2][SLAB] floats (double-buffered by minibatch parity) then
-// XCH_BLOCKS uint64 sequence flags; block b owns parameters [b XCH_SPAN, (b + 1) XCH_SPAN).
-enum : int { XCH_BLOCKS = 8, XCH_SPAN = (SLAB + XCH_BLOCKS - 1) / XCH_BLOCKS, XCH_MAX_RANKS = 8 };
+// One-shot gradient exchange over peer-mapped (IPC) memory, fused with the ordered block
+// reduction and Adam (wk_comm_init_ipc): rank r's exchange region is [2][SLAB] floats
+// (double-buffered by minibatch parity) then XCH_FLAGS uint64 sequence flags, one per block of
+// the fused kernel (each block owns a span of parameter quads).
+enum : int { XCH_FLAGS = 128, XCH_MAX_RANKS = 8 };
 struct XchArgs {
-  const float* grad;                   // this rank's ordered block reduction [SLAB]
+  const float* partial;                // this rank's gradient-kernel block slabs [nblocks][SLAB]
+  int nblocks;
   float* grad_out;                     // the rank-order sum over ranks [SLAB]
   float* slab[XCH_MAX_RANKS];          // every rank's exchange region (own + peer-mapped)
   uint64_t* flag[XCH_MAX_RANKS];       // every rank's XCH_BLOCKS flags
@@ -147,7 +149,7 @@ struct XchArgs {
   AdamArgs a;
 };
 size_t xch_region_bytes();
-hipError_t launch_xch_adam(const XchArgs& x, hipStream_t s);
+hipError_t launch_reduce_xch_adam(const XchArgs& x, hipStream_t s);
 hipError_t launch_normalize(float* x, int n, float eps, hipStream_t s);
 hipError_t launch_xavier(float* W, uint64_t seed, hipStream_t s);
 

@@ -483,30 +483,61 @@ hipError_t launch_grad_reduce_adam(const float* partial, int nblocks, float* par
                      grad, a);
   return hipGetLastError();
 }
-// One-shot exchange + Adam (wk_comm_init_ipc): the minibatch's gradient all-reduce without a
-// collective library.  Each rank publishes its ordered block sum into its own exchange region
-// (slab buffer seq & 1), releases a per-block sequence flag at system scope, waits (bounded)
-// until every peer's flag for the block reaches seq, and reads the peers' slabs directly
-// through the IPC mappings -- summing in rank order, rank 0's value first, which for two ranks
-// is the RCCL / host all-reduce's a + b bit for bit -- then applies Adam to its span of the
-// parameters.  Reuse of a buffer two minibatches later is safe: a rank publishes seq + 2 only
-// after its exchange of seq + 1 saw every peer's seq + 1 flag, which a peer sets only once
-// its own exchange of seq (the last read of the seq buffers) has completed (stream order).
-__global__ __launch_bounds__(256) void k_xch_adam(XchArgs x) {
-  const int b = blockIdx.x, t = threadIdx.x;
-  const int lo = b * XCH_SPAN, hi = lo + XCH_SPAN < SLAB ? lo + XCH_SPAN : SLAB;
+// One-shot exchange (wk_comm_init_ipc): the minibatch's gradient all-reduce without a
+// collective library, fused with the ordered block reduction and Adam -- one launch per
+// minibatch after the gradient kernel, as on one GPU.  Block b (the grid of k_grad_reduce_fused)
+// first forms this rank's ordered sum of its parameter quads exactly as k_grad_reduce_fused
+// does, publishes it into this rank's exchange region (slab buffer seq & 1) and releases its
+// sequence flag at system scope; it then waits (bounded) until every peer's flag b reaches
+// seq, reads the peers' values directly through the IPC mappings and sums the ranks in rank
+// order (rank 0's value first: for two ranks exactly the RCCL / host all-reduce's a + b), and
+// applies Adam.  A buffer is reused two minibatches later only: a rank publishes seq + 2 after
+// its exchange of seq + 1 saw every peer's seq + 1 flag, which a peer sets only once its own
+// exchange of seq -- the last read of the seq buffers -- has completed (stream order).
+__global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
+  __shared__ float4 gs[RG][QB];
+  const int qi = threadIdx.x % QB, gi = threadIdx.x / QB;
+  const int q = blockIdx.x * QB + qi;
+  const int ngroups = (x.nblocks + RG - 1) / RG;
+  const int p = 4 * q + gi;  // (gi < 4) this thread's parameter
+  const bool adam_lane = gi < 4 && p < NPARAM;
+  float m0 = 0.0f, v0 = 0.0f, w0 = 0.0f;
+  if (adam_lane) { m0 = x.a.m[p]; v0 = x.a.v[p]; w0 = x.a.W[p]; }
+  float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (q < SLAB / 4 && gi < ngroups) {  // stage 1, as k_grad_reduce_fused
+    const int b0 = gi * RG;
+    float4 v[RG];
+#pragma unroll
+    for (int j = 0; j < RG; j++)
+      v[j] = (b0 + j < x.nblocks) ? ((const float4*)(x.partial + (size_t)(b0 + j) * SLAB))[q]
+                                  : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int j = 0; j < RG; j++)
+      if (b0 + j < x.nblocks) {
+        acc.x = acc.x + v[j].x; acc.y = acc.y + v[j].y;
+        acc.z = acc.z + v[j].z; acc.w = acc.w + v[j].w;
+      }
+  }
+  gs[gi][qi] = acc;
+  __syncthreads();
   const int buf = (int)(x.seq & 1u);
-  float* const own = x.slab[x.rank] + (size_t)buf * SLAB;
-  for (int p = lo + t; p < hi; p += 256) own[p] = x.grad[p];
+  float mine = 0.0f;
+  if (gi < 4 && q < SLAB / 4) {  // stage 2: this rank's ordered sum, published
+    const float* gf = (const float*)gs;
+    for (int g = 0; g < ngroups; g++) mine = mine + gf[(g * QB + qi) * 4 + gi];
+    x.slab[x.rank][(size_t)buf * SLAB + p] = mine;
+  }
   __syncthreads();  // (workgroup release: every wave's stores have reached the L2)
+  const int t = threadIdx.x;
   if (t == 0)
-    __hip_atomic_store(x.flag[x.rank] + b, x.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (t < x.nranks && t != x.rank) {
-    uint64_t* f = x.flag[t] + b;
+    __hip_atomic_store(x.flag[x.rank] + blockIdx.x, x.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t < x.nranks && t != x.rank &&
+      __hip_atomic_load(x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+    const uint64_t* f = x.flag[t] + blockIdx.x;
     uint32_t spins = 0;
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < x.seq) {
-      if (++spins > (1u << 24)) {  // ~1 s: a peer is gone -- report, never hang the GPU
-        atomicOr(x.err, 1u);
+      if (++spins > (1u << 26)) {  // seconds: a peer is gone -- report, never hang the GPU (and
+        atomicOr(x.err, 1u);       // the next exchanges skip the wait once this is set)
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -514,17 +545,19 @@ __global__ __launch_bounds__(256) void k_xch_adam(XchArgs x) {
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale peer lines
-  for (int p = lo + t; p < hi; p += 256) {
-    float acc = x.rank == 0 ? x.grad[p] : x.slab[0][(size_t)buf * SLAB + p];
+  if (gi < 4 && q < SLAB / 4) {
+    float sum = x.rank == 0 ? mine : x.slab[0][(size_t)buf * SLAB + p];
     for (int r = 1; r < x.nranks; r++)
-      acc = acc + (r == x.rank ? x.grad[p] : x.slab[r][(size_t)buf * SLAB + p]);
-    x.grad_out[p] = acc;
-    if (p < NPARAM) adam_param(x.a, p, acc);
+      sum = sum + (r == x.rank ? mine : x.slab[r][(size_t)buf * SLAB + p]);
+    x.grad_out[p] = sum;
+    if (adam_lane) adam_apply(x.a, p, sum, m0, v0, w0);
   }
 }
-size_t xch_region_bytes() { return sizeof(float) * 2 * SLAB + sizeof(uint64_t) * XCH_BLOCKS; }
-hipError_t launch_xch_adam(const XchArgs& x, hipStream_t s) {
-  hipLaunchKernelGGL(k_xch_adam, dim3(XCH_BLOCKS), dim3(256), 0, s, x);
+size_t xch_region_bytes() { return sizeof(float) * 2 * SLAB + sizeof(uint64_t) * XCH_FLAGS; }
+hipError_t launch_reduce_xch_adam(const XchArgs& x, hipStream_t s) {
+  static_assert((SLAB / 4 + QB - 1) / QB <= XCH_FLAGS, "one flag per block");
+  if (x.nblocks > RG * RG) return hipErrorInvalidValue;  // (the gradient kernel caps at 256)
+  hipLaunchKernelGGL(k_reduce_xch_adam, dim3((SLAB / 4 + QB - 1) / QB), dim3(RG * QB), 0, s, x);
   return hipGetLastError();
 }
 

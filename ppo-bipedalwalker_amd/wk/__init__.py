@@ -40,6 +40,7 @@ EXPORTS = [
     "wk_episode_log_drain", "wk_loss_log_drain", "wk_write_data_file",
     "wk_comm_unique_id", "wk_comm_init", "wk_comm_init_host", "wk_allreduce_test", "wk_profile_enable",
     "wk_profile_get", "wk_profile_reset", "wk_count_events", "wk_snapshot", "wk_time_gradient",
+    "wk_comm_ipc_handle", "wk_comm_init_ipc",
 ]
 
 
@@ -233,6 +234,8 @@ def load_library(path=None):
         "wk_allreduce_test": (I, [P, P, I]),
         "wk_comm_init_host": (I, [P, I, I, HOST_ALLREDUCE_FN, P]),
         "wk_time_gradient": (I, [P, I, I, C.POINTER(C.c_double)]),
+        "wk_comm_ipc_handle": (I, [P, P]),
+        "wk_comm_init_ipc": (I, [P, I, I, P]),
         "wk_profile_enable": (I, [P, I]),
         "wk_profile_get": (I, [P, C.POINTER(Profile)]),
         "wk_profile_reset": (I, [P]),
@@ -669,6 +672,19 @@ class Engine:
         self._host_ar = HOST_ALLREDUCE_FN(_cb)
         self._chk(self.lib.wk_comm_init_host(self.h, int(rank), int(nranks), self._host_ar, None),
                   "wk_comm_init_host")
+
+    def comm_init_ipc(self, rank, nranks, allgather):
+        """wk_comm_ipc_handle + wk_comm_init_ipc: the one-shot exchange over peer-mapped memory.
+        `allgather(bytes) -> list of bytes` (rank order) exchanges the 64-byte IPC handles over
+        any control plane (e.g. torch.distributed.all_gather_object over gloo)."""
+        h = (C.c_uint8 * 64)()
+        self._chk(self.lib.wk_comm_ipc_handle(self.h, h), "wk_comm_ipc_handle")
+        handles = allgather(bytes(h))
+        if len(handles) != nranks or any(len(x) != 64 for x in handles):
+            raise WkError("wk_comm_init_ipc: need one 64-byte handle per rank")
+        buf = (C.c_uint8 * (64 * nranks)).from_buffer_copy(b"".join(handles))
+        self._chk(self.lib.wk_comm_init_ipc(self.h, int(rank), int(nranks), buf),
+                  "wk_comm_init_ipc")
 
     def allreduce_test(self, x):
         x = _f32(x).copy()

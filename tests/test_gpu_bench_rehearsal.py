@@ -23,12 +23,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_bench_two_rank_rehearsal():
+@pytest.mark.parametrize("exchange", ["rccl", "ipc"])
+def test_bench_two_rank_rehearsal(exchange):
+    """exchange rccl: with --rehearse the all-reduce goes over the host (gloo); ipc: the one-shot
+    exchange over IPC-mapped memory runs on the device, as it would on 8 GPUs"""
     cmd = ["timeout", "-k", "10", "240", sys.executable, "-m", "torch.distributed.run",
            "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
            "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2",
            "--steps", "2", "--warmup", "1", "--rehearse", "--walkers-global", "4096",
-           "--horizon", "8", "--epochs", "1", "--regime-iters", "1"]
+           "--horizon", "8", "--epochs", "1", "--regime-iters", "1", "--exchange", exchange]
     p = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     assert p.returncode == 0, p.stdout[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
@@ -37,6 +40,7 @@ def test_bench_two_rank_rehearsal():
     assert out["n_gpus"] == 2 and out["scaling"] == "strong" and "rehearsal" in out
     assert out["config"]["walkers_per_gpu"] == 2048 and out["config"]["global_walkers"] == 4096
     assert out["config"]["minibatch_global"] == 4096
+    assert out["config"]["exchange"] == ("ipc" if exchange == "ipc" else "host (gloo)")
     assert "quad" in out["roofline"]["kernel"]
     assert out["value"] > 0 and out["ms_per_step"] > 0
     assert abs(out["value"] - 4096 * 8 * 2 / (out["ms_per_step"] * 2e-3)) < 1e-6 * out["value"]

@@ -2,7 +2,11 @@
 
 RCCL refuses two ranks on one device, so the ranks' all-reduce goes through
 wk_comm_init_host (the same sequence: ordered block reduction -> all-reduce of the 6,153-float
-slab -> replicated Adam) with torch.distributed over gloo.  Each rank holds its contiguous
+slab -> replicated Adam) with torch.distributed over gloo -- and, as the second exchange, through
+the one-shot IPC exchange (wk_comm_init_ipc: each rank's slab published in its own
+peer-mapped region, read by the others, summed in rank order, Adam fused), which must give the
+host all-reduce's results bit for bit (two processes on one GPU still run on different XCDs'
+L2 caches: the system-scope release / acquire of the exchange is exercised).  Each rank holds its contiguous
 shard of the walkers (EnvOffset = rank x 256) and the global minibatch divisor; checked:
 
   * each rank's rollout equals a communicator-free context on the same shard (sharding by
@@ -46,7 +50,7 @@ def _adam_t1(w, g, alpha=np.float32(0.001), beta1=0.9, beta2=0.999, eps=np.float
     return w - ((mh / den) * alpha), m, v
 
 
-def test_two_ranks_host_allreduce(tmp_path):
+def _run_two_ranks(out, mode):
     port = _free_port()
     procs = []
     for r in range(2):
@@ -54,12 +58,23 @@ def test_two_ranks_host_allreduce(tmp_path):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen(
             ["timeout", "-k", "10", "240", sys.executable,
-             os.path.join(ROOT, "tests", "workers", "multirank_worker.py"), str(tmp_path)],
+             os.path.join(ROOT, "tests", "workers", "multirank_worker.py"), str(out), mode],
             env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = [p.communicate()[0] for p in procs]
     for p, o in zip(procs, outs):
         assert p.returncode == 0, o[-3000:]
-    r0, r1 = (np.load(tmp_path / f"rank{r}.npz") for r in range(2))
+    return [np.load(out / f"rank{r}.npz") for r in range(2)]
+
+
+@pytest.fixture(scope="module")
+def two_rank_runs(tmp_path_factory):
+    """both exchanges, each with two processes on GPU 0"""
+    return {mode: _run_two_ranks(tmp_path_factory.mktemp(mode), mode) for mode in ("host", "ipc")}
+
+
+@pytest.mark.parametrize("mode", ["host", "ipc"])
+def test_two_ranks_allreduce(two_rank_runs, mode):
+    r0, r1 = two_rank_runs[mode]
     for r in (r0, r1):
         assert r["same_traj"] and r["same_state"]
     np.testing.assert_array_equal(r0["w0"], r1["w0"])
@@ -73,7 +88,19 @@ def test_two_ranks_host_allreduce(tmp_path):
         assert float(r["cd"]) == np.float32(r0["cd_l"]) + np.float32(r1["cd_l"])
         assert float(r["ad"]) == np.float32(r0["ad_l"]) + np.float32(r1["ad_l"])
     np.testing.assert_array_equal(r0["w2"], r1["w2"])
+    np.testing.assert_array_equal(r0["w3"], r1["w3"])
+    assert int(r0["t3"]) == int(r1["t3"]) == 2 + 2 * 3 * 4
     assert not np.array_equal(r0["state"], r1["state"])  # different shards
+
+
+def test_ipc_exchange_equals_host_allreduce(two_rank_runs):
+    """the one-shot IPC exchange (peer-mapped slabs, rank-order sum, fused Adam) gives the host
+    all-reduce's weights and Adam moments bit for bit -- through 26 Adam steps with several
+    minibatches and epochs per update (sequence numbers, double-buffered slabs)"""
+    for h, i in zip(two_rank_runs["host"], two_rank_runs["ipc"]):
+        for k in ("w1", "m1", "v1", "w2", "w3", "m3", "v3", "state"):
+            np.testing.assert_array_equal(h[k], i[k], err_msg=k)
+        assert float(h["cd"]) == float(i["cd"]) and float(h["ad"]) == float(i["ad"])
 
 
 def test_failing_host_allreduce_is_reported(wk):

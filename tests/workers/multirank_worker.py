@@ -1,7 +1,8 @@
 """One rank of tests/test_gpu_multirank.py: RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT from
 the environment, gloo control plane, a libwk context on GPU 0 whose minibatch all-reduce goes
 through wk_comm_init_host -> torch.distributed.all_reduce (RCCL refuses two ranks on one
-device).  Writes its results to <out>/rank<r>.npz."""
+device) or, with argv[2] = ipc, through the one-shot exchange over IPC-mapped memory
+(wk_comm_init_ipc).  Writes its results to <out>/rank<r>.npz."""
 import os
 import sys
 
@@ -16,6 +17,7 @@ from wk.dist import env_from_launcher, make_shard  # noqa: E402
 
 SEED = 20250905
 out_dir = sys.argv[1]
+mode = sys.argv[2] if len(sys.argv) > 2 else "host"  # host all-reduce (gloo) or the IPC exchange
 n_local, T = 256, 8
 rank, world, _ = env_from_launcher()
 dist.init_process_group("gloo")
@@ -31,7 +33,14 @@ def allreduce(a):
 
 eng = wk.Engine(n_local, seed=SEED, **cfg)
 solo = wk.Engine(n_local, seed=SEED, **cfg)  # same shard, no communicator
-eng.comm_init_host(rank, world, allreduce)
+if mode == "ipc":
+    def allgather(b):
+        out = [None] * world
+        dist.all_gather_object(out, b)
+        return out
+    eng.comm_init_ipc(rank, world, allgather)
+else:
+    eng.comm_init_host(rank, world, allreduce)
 w0 = eng.get_weights()
 eng.rollout(T)
 solo.rollout(T)
@@ -56,7 +65,16 @@ m1, v1, t1 = eng.get_adam()
 eng.rollout(T)  # a second iteration: the replicas stay identical
 eng.ppo_update(update_index=1)
 w2 = eng.get_weights()
+# several minibatches and epochs per update (the exchange's sequence numbers and double
+# buffering): 3 epochs x 4 minibatches, twice
+for u in (2, 3):
+    eng.rollout(T)
+    eng.ppo_update(epochs=3, minibatch=shard.minibatch_local // 4,
+                   minibatch_global=shard.minibatch_global // 4, update_index=u)
+w3 = eng.get_weights()
+m3, v3, t3 = eng.get_adam()
 np.savez(os.path.join(out_dir, f"rank{rank}.npz"), w0=w0, w1=w1, m1=m1, v1=v1, t1=t1, w2=w2,
+         w3=w3, m3=m3, v3=v3, t3=t3,
          g_local=g_local, cd=cd, ad=ad, cd_l=cd_l, ad_l=ad_l, same_traj=same_traj,
          same_state=same_state, state=eng.get_state())
 eng.close()
