@@ -35,6 +35,7 @@ enum ProfKind { PK_PHYS = 0, PK_GRAD, PK_REDUCE, PK_ADAM, PK_ALLRED, PK_RET, PK_
 
 struct wk_ctx {
   wk_config cfg;
+  int grad_impl = -1;  // matrix-core gradient kernel (wk::GI_*; -1 = by minibatch size)
   int device = 0;
   int n = 0;
   uint64_t seed = 0;
@@ -302,6 +303,7 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   // > 64 KiB dynamic LDS for the gradient kernels, set on this device (the attribute is
   // per device; wk_create is the only place, so launches never race on it)
   if (wk::configure_device_kernels() != hipSuccess) { x->err = "hipFuncSetAttribute failed"; return fail(WK_ERR_HIP); }
+  x->grad_impl = wk::grad_impl_env();
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) {
     x->err = "hipStreamCreate failed";
     return fail(WK_ERR_HIP);
@@ -974,7 +976,8 @@ int wk_set_trajectory(wk_ctx* c, int horizon, const float* s, const float* a, co
 // wpb == 0: the matrix-core kernel (wk_ppo_mfma.hip); wpb >= 1: the lane-per-neuron
 // kernel (wk_ppo.hip; wpb == 1 visits the samples in minibatch order)
 static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
-  const int nblocks = wpb == 0 ? wk::ppo_grad_mfma_blocks(g.samples)
+  const int gi = wk::grad_impl_for(c->grad_impl, g.samples);
+  const int nblocks = wpb == 0 ? wk::ppo_grad_mfma_blocks(g.samples, gi)
                                : (g.samples + wpb * g.spw - 1) / (wpb * g.spw);
   // block slabs followed by the stage-1 group sums of the ordered reduction
   const size_t need = ((size_t)nblocks + wk::grad_reduce_groups(nblocks)) * wk::SLAB;
@@ -988,7 +991,7 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   g.partial = c->partial;
   {
     ProfScope ps(c, PK_GRAD, 0, 2);
-    HIPCHK(c, wpb == 0 ? wk::launch_ppo_grad_mfma(g, nblocks, c->stream)
+    HIPCHK(c, wpb == 0 ? wk::launch_ppo_grad_mfma(g, nblocks, gi, c->stream)
                        : wk::launch_ppo_grad(g, wpb, nblocks, c->stream));
   }
   wk::AdamArgs a{};
@@ -1093,7 +1096,8 @@ int wk_time_gradient(wk_ctx* c, int minibatch, int reps, double* ms_per_launch) 
   g.b_div = (float)(c->cfg.MinibatchGlobal > 0 ? c->cfg.MinibatchGlobal : M);
   g.pk = wk::perm_key(c->seed, 0u, 0u, pool);
   g.base = 0;
-  const int nblocks = wk::ppo_grad_mfma_blocks(M);
+  const int gi = wk::grad_impl_for(c->grad_impl, M);
+  const int nblocks = wk::ppo_grad_mfma_blocks(M, gi);
   const size_t need = ((size_t)nblocks + wk::grad_reduce_groups(nblocks)) * wk::SLAB;
   if (c->partial_floats < need) {
     if (c->partial) (void)hipFree(c->partial);
@@ -1106,9 +1110,9 @@ int wk_time_gradient(wk_ctx* c, int minibatch, int reps, double* ms_per_launch) 
   hipEvent_t a = nullptr, b = nullptr;
   HIPCHK(c, hipEventCreate(&a));
   HIPCHK(c, hipEventCreate(&b));
-  HIPCHK(c, wk::launch_ppo_grad_mfma(g, nblocks, c->stream));  // warm
+  HIPCHK(c, wk::launch_ppo_grad_mfma(g, nblocks, gi, c->stream));  // warm
   HIPCHK(c, hipEventRecord(a, c->stream));
-  for (int i = 0; i < reps; i++) HIPCHK(c, wk::launch_ppo_grad_mfma(g, nblocks, c->stream));
+  for (int i = 0; i < reps; i++) HIPCHK(c, wk::launch_ppo_grad_mfma(g, nblocks, gi, c->stream));
   HIPCHK(c, hipEventRecord(b, c->stream));
   HIPCHK(c, hipEventSynchronize(b));
   float ms = 0.0f;

@@ -121,10 +121,15 @@ hipError_t launch_returns(int n, int T, int use_gae, float gamma, float lambda, 
 hipError_t launch_ppo_grad(const GradArgs& g, int wpb, int nblocks, hipStream_t s);
 hipError_t configure_device_kernels();  // dynamic-LDS attributes, current device (wk_create)
 hipError_t configure_mfma_kernels();
-hipError_t launch_ppo_grad_mfma(const GradArgs& g, int nblocks, hipStream_t s);
+// matrix-core gradient kernels: producer / consumer pairs (ws), tile-parallel teams of four
+// waves, two (tp) or one (tp1) per block, one wave per chunk (mf); GI_AUTO picks by size
+enum : int { GI_AUTO = -1, GI_WS = 0, GI_TP2 = 1, GI_TP1 = 2, GI_MF = 3 };
+int grad_impl_env();                       // WK_GRAD_IMPL = ws / tp / tp1 / mf, else GI_AUTO
+int grad_impl_for(int impl, int samples);  // resolves GI_AUTO
+hipError_t launch_ppo_grad_mfma(const GradArgs& g, int nblocks, int impl, hipStream_t s);
 hipError_t launch_swizzle(const float* W, float* Wz, hipStream_t s);
 int mfma_image_floats();
-int ppo_grad_mfma_blocks(int samples);
+int ppo_grad_mfma_blocks(int samples, int impl);
 hipError_t launch_grad_reduce(const float* partial, int nblocks, float* part2, float* grad,
                               hipStream_t s);
 int grad_reduce_groups(int nblocks);

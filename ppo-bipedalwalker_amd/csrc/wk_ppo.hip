@@ -368,8 +368,12 @@ __global__ __launch_bounds__(RG * QB) void k_grad_reduce_fused(const float* __re
   if (gi < 4 && q < SLAB / 4) {  // one parameter per thread: component gi of quad qi
     const float* gf = (const float*)gs;
     const int p = 4 * q + gi;
-    float t = 0.0f;
-    for (int g = 0; g < ngroups; g++) t = t + gf[(g * QB + qi) * 4 + gi];
+    float gv[RG], t = 0.0f;  // (all RG reads issued before the ordered adds)
+#pragma unroll
+    for (int g = 0; g < RG; g++) gv[g] = gf[(g * QB + qi) * 4 + gi];
+#pragma unroll
+    for (int g = 0; g < RG; g++)
+      if (g < ngroups) t = t + gv[g];
     grad[p] = t;
     if (adam_lane) adam_apply(a, p, t, m0, v0, w0);
   }
@@ -524,7 +528,12 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
   float mine = 0.0f;
   if (gi < 4 && q < SLAB / 4) {  // stage 2: this rank's ordered sum, published
     const float* gf = (const float*)gs;
-    for (int g = 0; g < ngroups; g++) mine = mine + gf[(g * QB + qi) * 4 + gi];
+    float gv[RG];
+#pragma unroll
+    for (int g = 0; g < RG; g++) gv[g] = gf[(g * QB + qi) * 4 + gi];
+#pragma unroll
+    for (int g = 0; g < RG; g++)
+      if (g < ngroups) mine = mine + gv[g];
     x.slab[x.rank][(size_t)buf * SLAB + p] = mine;
   }
   __syncthreads();  // (workgroup release: every wave's stores have reached the L2)

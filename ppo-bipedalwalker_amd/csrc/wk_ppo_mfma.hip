@@ -25,6 +25,9 @@
 // 80 = 16 mod 64 banks: conflict-free operand reads).  Accumulators stay in registers
 // across chunks; waves fold into the block slab in wave order and blocks write partial
 // slabs for the ordered reduction (bit-reproducible, no atomics).
+#include <cstdlib>
+#include <cstring>
+
 #include "wk_common.h"
 #include "wk_kernels.h"
 #include "wk_mfma_layout.h"
@@ -991,6 +994,382 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// k_ppo_grad_tp: the same minibatch gradient with the neurons of one chunk split over the four
+// waves of a team ("tile-parallel").  k_ppo_grad_ws runs a chunk's 248 MFMAs and its loss chain
+// on one SIMD, so a launch is at least one chunk's serial latency plus the weight staging: at a
+// strong-scaling shard (8,192 samples = 512 chunks, one per SIMD pair) that is 15 us for 1.9 us
+// of matrix work.  Here wave w of a team owns neuron tile w (neurons 16 w .. 16 w + 15 of every
+// 64-wide layer) and with it a disjoint quarter of the parameters:
+//   layer 1   z1 / zc1 of tile w                         (6 MFMAs, K 12)
+//   layer 2   z2 of tile w = W2[tile w][:] H1            (16 MFMAs, B = H1 tile from LDS)
+//   rows      z3 / V partial dots over the tile's 16 neurons, summed over the team in LDS
+//   loss      every wave, redundantly (the same values in all four)
+//   VALU      dW3 / dWc2 / db2 partials and gz2 / gzc1 of tile w
+//   backward  dW2[tile w][:] += gz2^T H1                 (16 MFMAs)
+//             gh1 of tile w = W2[:][tile w]^T gz2        (16 MFMAs, B = G2 tile from LDS)
+//             dW1 | db1, dWc1 | dbc1 rows of tile w      (8 MFMAs)
+// 62 MFMAs per wave and chunk, three team barriers, weights in registers straight from the
+// image (no LDS staging).  Every accumulator's k order is the one k_ppo_grad_ws uses; only the
+// z3 / V dots are associated per tile.  A block holds TEAMS teams on separate chunks (two waves
+// per SIMD); the teams' slabs are folded in team order.  Each wave writes its own parameters,
+// so a one-team block needs no fold at all.
+namespace tp {
+enum : int {
+  RT = 68, T68 = 16 * RT, RSX = 20, TSX = 16 * RSX, RP = 80,  // P: [wave 4][d 5][16 samples]
+  O_SX = 0, O_H1 = TSX, O_G2 = O_H1 + T68, O_GC1 = O_G2 + T68, O_G1 = O_GC1 + T68,
+  O_P = O_G1 + T68, TB = O_P + 4 * RP
+};
+static_assert(TB % 4 == 0, "16-byte aligned tiles");
+template <int TEAMS> struct L {
+  enum : int { LOOP = TEAMS * 2 * TB, FLOATS = LOOP > TEAMS * SLAB ? LOOP : TEAMS * SLAB };
+  static_assert(FLOATS * 4 <= 160 * 1024, "fits the CU's LDS");
+};
+}  // namespace tp
+
+#ifndef WK_SLAB_SC1
+#define WK_SLAB_SC1 1
+#endif
+template <int TEAMS>
+__global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
+  using namespace mf;
+  using namespace tp;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int team = wv >> 2, w = wv & 3;
+  const int n = lane & 15, g = lane >> 4;
+#ifdef WK_GRAD_NOLOOP  // probe: the launch without its chunk loop (fixed-cost measurement)
+  const int nchunks = 0;
+#else
+  const int nchunks = (ga.samples + 15) / 16;
+#endif
+  const int nt = gridDim.x * TEAMS;
+  const int c0 = blockIdx.x * TEAMS + team;
+  const int kp = c0 < nchunks ? (nchunks - 1 - c0) / nt + 1 : 0;  // this team's chunks
+  const int kmax = blockIdx.x * TEAMS < nchunks ? (nchunks - 1 - blockIdx.x * TEAMS) / nt + 1 : 0;
+  const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+#ifdef WK_GRAD_PROF
+  uint64_t gp[12] = {}, gp_t = __builtin_amdgcn_s_memtime();
+#endif
+
+  // gather (CreateBatches, PPOAgent.cs:512-533): lane (n, g) holds features g, 4 + g, 8 + g of
+  // sample n (layer 1's B operand) and the sample's action dim g entries
+  struct Smp { float s[3]; float act, lpo, ret, adv; };
+  auto gather = [&](int c) {
+    Smp m;
+    const int pos = c * 16 + n;
+    uint32_t idx = ga.base + (uint32_t)(pos < ga.samples ? pos : 0);
+    if (ga.use_perm) idx = perm_apply(idx, ga.pk);
+#pragma unroll
+    for (int t = 0; t < 3; t++) m.s[t] = ga.states[(size_t)idx * 12 + 4 * t + g];
+    m.act = ga.actions[(size_t)idx * 4 + g];
+    m.lpo = ga.logp_old[(size_t)idx * 4 + g];
+    m.ret = ga.returns[idx];
+    m.adv = ga.adv[idx];
+    return m;
+  };
+  Smp nxt = gather(c0 < nchunks ? c0 : 0);
+
+  // this wave's weights (image order, wk_mfma_layout.h), loaded once into registers
+  float wa1[3], wc1[3];
+  f4 w2f[4], w2b[4], w3[4];
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    wa1[t] = ga.Wz[AW1F + (w * 3 + t) * 64 + lane];
+    wc1[t] = ga.Wz[CW1F + (w * 3 + t) * 64 + lane];
+  }
+#pragma unroll
+  for (int M = 0; M < 4; M++) {
+    w2f[M] = *(const f4*)(ga.Wz + W2F + ((w * 4 + M) * 64 + lane) * 4);
+    w2b[M] = *(const f4*)(ga.Wz + W2B + ((w * 4 + M) * 64 + lane) * 4);
+  }
+#pragma unroll
+  for (int d = 0; d < 4; d++) w3[d] = *(const f4*)(ga.Wz + W3 + d * 64 + 16 * w + 4 * g);
+  const f4 wc2 = *(const f4*)(ga.Wz + WC2 + 16 * w + 4 * g);
+  const f4 ba1 = *(const f4*)(ga.Wz + BA1 + 16 * w + 4 * g);
+  const f4 bc1 = *(const f4*)(ga.Wz + BC1 + 16 * w + 4 * g);
+  const f4 ba2 = *(const f4*)(ga.Wz + BA2 + 16 * w + 4 * g);
+  const float b3g = ga.Wz[BA3 + g], bc2 = ga.Wz[BC2];
+
+  float* const tt = lds + team * 2 * TB;  // this team's two chunk buffers
+  // the SX tiles' constant columns: 12 = 1.0 (the bias column), 13..15 = 0
+  if (w == 0 && g == 0) {
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+      *(f4*)(tt + b * TB + O_SX + n * RSX + 12) = f4{1.0f, 0.0f, 0.0f, 0.0f};
+  }
+
+  GP_MARK(0);  // prologue: weights issued, first gather issued
+  f4 a2[4], aw3[4], a1 = z4, a1c = z4, awc2 = z4, db2 = z4;
+#pragma unroll
+  for (int i = 0; i < 4; i++) { a2[i] = z4; aw3[i] = z4; }
+  float db3 = 0.0f, dbc2 = 0.0f, diagC = 0.0f, diagA = 0.0f, skipped = 0.0f;
+
+#pragma unroll 1
+  for (int i = 0; i < kmax; i++) {
+    const bool live = i < kp;  // team-uniform; a finished team still meets the barriers
+    const int c = c0 + i * nt;
+    float* const tb = tt + (i & 1) * TB;
+    const Smp cur = nxt;
+    if (i + 1 < kp) nxt = gather(c + nt);
+    const bool valid = c * 16 + n < ga.samples;
+    f4 h1 = z4, hc1 = z4;
+    if (live) {
+      if (w == 0) {
+#pragma unroll
+        for (int t = 0; t < 3; t++) tb[O_SX + n * RSX + 4 * t + g] = cur.s[t];
+      }
+      // ---- layer 1 of tile w ----
+      f4 z1 = z4, zc1 = z4;
+#pragma unroll
+      for (int t = 0; t < 3; t++) {
+        z1 = mfma(wa1[t], cur.s[t], z1);
+        zc1 = mfma(wc1[t], cur.s[t], zc1);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        h1[r] = mf_lrelu(z1[r] + ba1[r]);
+        hc1[r] = mf_lrelu(zc1[r] + bc1[r]);
+      }
+      *(f4*)(tb + O_H1 + n * RT + 16 * w + 4 * g) = h1;
+    }
+    GP_MARK(1);  // layer 1
+    __syncthreads();  // B1: the team's H1 tile
+    GP_MARK(2);
+    f4 h2 = z4;
+    if (live) {
+      // ---- layer 2 of tile w (k order (Mp, r), as k_ppo_grad_ws) ----
+      f4 hb[4];
+#pragma unroll
+      for (int Mp = 0; Mp < 4; Mp++) hb[Mp] = *(const f4*)(tb + O_H1 + n * RT + 16 * Mp + 4 * g);
+      f4 z2 = z4;
+#pragma unroll
+      for (int Mp = 0; Mp < 4; Mp++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) z2 = mfma(w2f[Mp][r], hb[Mp][r], z2);
+#pragma unroll
+      for (int r = 0; r < 4; r++) h2[r] = mf_lrelu(z2[r] + ba2[r]);
+      // ---- the output rows' partial dots over the tile ----
+      float p3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, pv = 0.0f;
+#pragma unroll
+      for (int d = 0; d < 4; d++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) p3[d] = __builtin_fmaf(w3[d][r], h2[r], p3[d]);
+#pragma unroll
+      for (int r = 0; r < 4; r++) pv = __builtin_fmaf(wc2[r], hc1[r], pv);
+#pragma unroll
+      for (int d = 0; d < 4; d++) {
+        p3[d] = p3[d] + __shfl_xor(p3[d], 16);
+        p3[d] = p3[d] + __shfl_xor(p3[d], 32);
+      }
+      pv = pv + __shfl_xor(pv, 16);
+      pv = pv + __shfl_xor(pv, 32);
+      // lane (n, g) stores dim g's partial, lanes of group 0 also V's
+      tb[O_P + w * RP + g * 16 + n] = g == 0 ? p3[0] : g == 1 ? p3[1] : g == 2 ? p3[2] : p3[3];
+      if (g == 0) tb[O_P + w * RP + 64 + n] = pv;
+    }
+    GP_MARK(3);  // layer 2 + rows
+    __syncthreads();  // B2: the team's partial dots
+    GP_MARK(4);
+    if (live) {
+      float z3 = 0.0f, pv = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        z3 = z3 + tb[O_P + q * RP + g * 16 + n];
+        pv = pv + tb[O_P + q * RP + 64 + n];
+      }
+      z3 = z3 + b3g;
+      const float V = pv + bc2;
+      // ---- PPO derivative for action dimension d = g (PPOAgent.cs:234-326) ----
+      const float act = cur.act, lpo = cur.lpo, ret = cur.ret, adv = cur.adv;
+      const float mean = tanhf(z3);
+      float criticLoss = 2.0f * (V - ret);
+      float fr = (act - mean) / ga.std_;
+      fr *= fr;
+      fr /= 2.0f;
+      const float lp = ga.lp_const - fr;
+      const float rr = expf(lp - lpo);
+      const float cr = rr >= ga.upper ? ga.upper : (rr <= ga.lower ? ga.lower : rr);
+      const float cra = cr * adv, ra = rr * adv;
+      const float partA = (ra <= cra ? 1.0f : 0.0f) * adv;
+      const float partB = (cra < ra ? 1.0f : 0.0f) * adv;
+      const float partC = (rr >= ga.lower && rr <= ga.upper) ? 1.0f : 0.0f;
+      float l = partA + (partB * partC);
+      l = l * -1.0f;
+      const float eo = expf(lpo);
+      float zd = eo == 0.0f ? 1.0f : 0.0f;  // Matrix.HadamardDivision throws -> sample skipped
+      zd = fmaxf(zd, __shfl_xor(zd, 16));
+      zd = fmaxf(zd, __shfl_xor(zd, 32));
+      const bool use = valid && zd == 0.0f;
+      const float lcd = l / eo;
+      const float prob = expf(lp);
+      const float frac = (act - mean) / (ga.std_ * ga.std_);
+      float actorLoss = (prob * frac) * lcd;
+      criticLoss = use ? criticLoss / ga.b_div : 0.0f;
+      actorLoss = use ? actorLoss / ga.b_div : 0.0f;
+      const float th = mean;  // tanh(z3) again in the reference's backward pass
+      const float gz3 = actorLoss * (1.0f - (th * th));
+      float q[4];
+#pragma unroll
+      for (int d = 0; d < 4; d++) q[d] = __shfl(gz3, n + 16 * d);
+      if (w == 0) {  // the sample-level terms, once per team
+        float al[4];
+#pragma unroll
+        for (int d = 0; d < 4; d++) al[d] = __shfl(actorLoss, n + 16 * d);
+        if (g == 0) {
+          diagC += criticLoss;
+          diagA += use ? ((((0.0f + al[0]) + al[1]) + al[2]) + al[3]) / 4.0f : 0.0f;
+          skipped += (valid && !use) ? 1.0f : 0.0f;
+          dbc2 += criticLoss;
+        }
+        db3 += gz3;
+      }
+      // ---- dW3 / dWc2 partials, gz2 / gzc1 of tile w ----
+      f4 gz2, gzc1;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+#pragma unroll
+        for (int d = 0; d < 4; d++) aw3[d][r] = __builtin_fmaf(q[d], h2[r], aw3[d][r]);
+        awc2[r] = __builtin_fmaf(criticLoss, hc1[r], awc2[r]);
+        float gh = 0.0f;
+#pragma unroll
+        for (int d = 0; d < 4; d++) gh = __builtin_fmaf(w3[d][r], q[d], gh);
+        gz2[r] = gh * mf_dlrelu(h2[r]);
+        gzc1[r] = (0.0f + wc2[r] * criticLoss) * mf_dlrelu(hc1[r]);
+      }
+      db2 = db2 + gz2;
+      *(f4*)(tb + O_G2 + n * RT + 16 * w + 4 * g) = gz2;
+      *(f4*)(tb + O_GC1 + n * RT + 16 * w + 4 * g) = gzc1;
+    }
+    GP_MARK(5);  // loss + VALU gradients
+    __syncthreads();  // B3: the team's G2 tile
+    GP_MARK(6);
+    if (live) {
+      // ---- dW2[tile w][:] += gz2^T H1 (samples on K: step r = samples 4 g + r) ----
+      {
+        float ag[4], bh[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          ag[r] = tb[O_G2 + (4 * g + r) * RT + 16 * w + n];
+#pragma unroll
+          for (int Nk = 0; Nk < 4; Nk++) bh[r][Nk] = tb[O_H1 + (4 * g + r) * RT + 16 * Nk + n];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int Nk = 0; Nk < 4; Nk++) a2[Nk] = mfma(ag[r], bh[r][Nk], a2[Nk]);
+      }
+      // ---- gh1 of tile w = W2[:][tile w]^T gz2 (B = the G2 tile) -> gz1 ----
+      f4 gb[4];
+#pragma unroll
+      for (int Mj = 0; Mj < 4; Mj++) gb[Mj] = *(const f4*)(tb + O_G2 + n * RT + 16 * Mj + 4 * g);
+      f4 gh1 = z4;
+#pragma unroll
+      for (int Mj = 0; Mj < 4; Mj++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) gh1 = mfma(w2b[Mj][r], gb[Mj][r], gh1);
+      f4 gz1;
+#pragma unroll
+      for (int r = 0; r < 4; r++) gz1[r] = gh1[r] * mf_dlrelu(h1[r]);  // lrelu(z) < 0 iff z < 0
+      *(f4*)(tb + O_G1 + n * RT + 16 * w + 4 * g) = gz1;  // this wave's columns only
+      wave_sync();
+      // ---- dW1 | db1, dWc1 | dbc1 rows of tile w += gz1^T [S | 1] ----
+      float bx[4], av[4], acv[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        bx[r] = tb[O_SX + (4 * g + r) * RSX + n];
+        av[r] = tb[O_G1 + (4 * g + r) * RT + 16 * w + n];
+        acv[r] = tb[O_GC1 + (4 * g + r) * RT + 16 * w + n];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        a1 = mfma(av[r], bx[r], a1);
+        a1c = mfma(acv[r], bx[r], a1c);
+      }
+    }
+    GP_MARK(7);  // backward
+  }
+
+  // ---- totals over the 16 sample lanes of each row, then this wave's part of the slab ----
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    db2[r] = row_sum16(db2[r]);
+    awc2[r] = row_sum16(awc2[r]);
+#pragma unroll
+    for (int d = 0; d < 4; d++) aw3[d][r] = row_sum16(aw3[d][r]);
+  }
+  db3 = row_sum16(db3);
+  dbc2 = row_sum16(dbc2);
+  diagC = row_sum16(diagC);
+  diagA = row_sum16(diagA);
+  skipped = row_sum16(skipped);
+  GP_MARK(8);  // row sums
+  // each team's slab in LDS in parameter order (every entry written by exactly one wave of
+  // the team), then the block writes (t0 [+ t1]) with 16-byte coalesced stores
+  __syncthreads();  // every wave is done with the tiles
+  float* const slab = lds + team * SLAB;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int j = 16 * w + 4 * g + r;
+#pragma unroll
+    for (int Nk = 0; Nk < 4; Nk++) slab[OFF_A_W2 + j * 64 + 16 * Nk + n] = a2[Nk][r];
+    if (n < 12) {
+      slab[OFF_A_W1 + j * 12 + n] = a1[r];
+      slab[OFF_C_W1 + j * 12 + n] = a1c[r];
+    } else if (n == 12) {
+      slab[OFF_A_B1 + j] = a1[r];
+      slab[OFF_C_B1 + j] = a1c[r];
+    } else if (n == 13) {
+      slab[OFF_A_B2 + j] = db2[r];
+      slab[OFF_C_W2 + j] = awc2[r];
+    } else if (n == 14) {
+#pragma unroll
+      for (int d = 0; d < 4; d++) slab[OFF_A_W3 + d * 64 + j] = aw3[d][r];
+    }
+  }
+  if (w == 0) {
+    if (n == 15) slab[OFF_A_B3 + g] = db3;
+    if (lane == 0) {
+      slab[OFF_C_B2] = dbc2;
+      slab[NPARAM] = diagC;
+      slab[NPARAM + 1] = diagA;
+      slab[NPARAM + 2] = skipped;
+    }
+    if (lane < SLAB - (NPARAM + 3)) slab[NPARAM + 3 + lane] = 0.0f;  // (the pads)
+  }
+  __syncthreads();
+  {
+    // written through to memory (sc1): the kernel-end release then has no dirty slab lines to
+    // write back out of the L2 (the ordered reduction reads them from another XCD anyway)
+    f4* const out = (f4*)(ga.partial + (size_t)blockIdx.x * SLAB);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, SLAB * 4, 0x00020000);
+    constexpr int NV = SLAB / 4, PER = (NV + 256 * TEAMS - 1) / (256 * TEAMS);
+    f4 sv[PER][TEAMS];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const int i = tid + k * 256 * TEAMS;
+#pragma unroll
+      for (int t = 0; t < TEAMS; t++) sv[k][t] = i < NV ? ((const f4*)(lds + t * SLAB))[i] : z4;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const int i = tid + k * 256 * TEAMS;
+      f4 acc = sv[k][0];
+      if (TEAMS == 2) acc = acc + sv[k][TEAMS - 1];
+#if WK_SLAB_SC1
+      typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+      if (i < NV) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc), rsrc, i * 16, 0, 16);
+#else
+      (void)rsrc;
+      if (i < NV) out[i] = acc;
+#endif
+    }
+  }
+  GP_MARK(9);  // slab
+  GP_FLUSH();
+}
+
 // the weight image from the flat parameters (initialisation, wk_set_weights)
 __global__ void k_swizzle(const float* __restrict__ W, float* __restrict__ Wz) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1013,28 +1392,60 @@ hipError_t launch_swizzle(const float* W, float* Wz, hipStream_t s) {
   return hipGetLastError();
 }
 
-#ifndef WK_GRAD_WS
-#define WK_GRAD_WS 1
-#endif
+// Which matrix-core gradient kernel (WK_GRAD_IMPL = ws / tp / tp1 / mf, read per context at
+// wk_create; default: by minibatch size).  The tile-parallel kernel has the shorter chain per
+// chunk, the producer / consumer kernel the higher throughput once every SIMD pair has several
+// chunks (measured, scripts/grad_impls.py: tp faster up to 24,576 samples, ws from 32,768).
+int grad_impl_env() {
+  if (const char* e = getenv("WK_GRAD_IMPL")) {
+    if (!strcmp(e, "ws")) return GI_WS;
+    if (!strcmp(e, "tp")) return GI_TP2;
+    if (!strcmp(e, "tp1")) return GI_TP1;
+    if (!strcmp(e, "mf")) return GI_MF;
+  }
+  return GI_AUTO;
+}
+int grad_impl_for(int impl, int samples) {
+  if (impl != GI_AUTO) return impl;
+  return samples < 32768 ? GI_TP2 : GI_WS;
+}
 hipError_t configure_mfma_kernels() {
   hipError_t e = hipFuncSetAttribute((const void*)k_ppo_grad_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)(sizeof(float) * mf::LDS_FLOATS));
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)k_ppo_grad_ws, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)(sizeof(float) * ws::LDS_FLOATS));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_ppo_grad_ws, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(sizeof(float) * ws::LDS_FLOATS));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_ppo_grad_tp<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(sizeof(float) * tp::L<2>::FLOATS));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_ppo_grad_tp<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(sizeof(float) * tp::L<1>::FLOATS));
+  return e;
 }
 
-int ppo_grad_mfma_blocks(int samples) {
+// blocks of the kernel `impl` (resolved) for a minibatch; at most 256 (one per CU; the ordered
+// reduction's one-launch form and the IPC exchange take up to 256 slabs)
+int ppo_grad_mfma_blocks(int samples, int impl) {
   const int chunks = (samples + 15) / 16;
-  int blocks = (chunks + mf::WAVES - 1) / mf::WAVES;
-  return blocks < 256 ? blocks : 256;  // one block per CU; waves loop over the chunks
+  const int per = impl == GI_TP2 ? 2 : impl == GI_TP1 ? 1 : mf::WAVES;
+  const int blocks = (chunks + per - 1) / per;
+  return blocks < 256 ? (blocks > 0 ? blocks : 1) : 256;
 }
 
-hipError_t launch_ppo_grad_mfma(const GradArgs& g, int nblocks, hipStream_t s) {
-  if (WK_GRAD_WS) {
-    hipLaunchKernelGGL(k_ppo_grad_ws, dim3(nblocks), dim3(64 * 2 * ws::PAIRS), sizeof(float) * ws::LDS_FLOATS, s, g);
-  } else {
-    hipLaunchKernelGGL(k_ppo_grad_mfma, dim3(nblocks), dim3(64 * mf::WAVES), sizeof(float) * mf::LDS_FLOATS, s, g);
+hipError_t launch_ppo_grad_mfma(const GradArgs& g, int nblocks, int impl, hipStream_t s) {
+  switch (impl) {
+    case GI_WS:
+      hipLaunchKernelGGL(k_ppo_grad_ws, dim3(nblocks), dim3(64 * 2 * ws::PAIRS), sizeof(float) * ws::LDS_FLOATS, s, g);
+      break;
+    case GI_TP1:
+      hipLaunchKernelGGL(k_ppo_grad_tp<1>, dim3(nblocks), dim3(256), sizeof(float) * tp::L<1>::FLOATS, s, g);
+      break;
+    case GI_MF:
+      hipLaunchKernelGGL(k_ppo_grad_mfma, dim3(nblocks), dim3(64 * mf::WAVES), sizeof(float) * mf::LDS_FLOATS, s, g);
+      break;
+    default:
+      hipLaunchKernelGGL(k_ppo_grad_tp<2>, dim3(nblocks), dim3(512), sizeof(float) * tp::L<2>::FLOATS, s, g);
   }
   return hipGetLastError();
 }

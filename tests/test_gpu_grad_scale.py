@@ -59,6 +59,26 @@ def test_minibatch_gradient_multichunk_vs_oracle(wk, orc, B, skip_at):
     assert cd == pytest.approx(ocd, rel=2e-4, abs=1e-6) and ad == pytest.approx(oad, rel=2e-4, abs=1e-6)
 
 
+@pytest.mark.parametrize("impl", ["ws", "tp", "tp1", "mf"])
+@pytest.mark.parametrize("B,skip_at", [(8192, 77), (20011, 20010), (600, None)])
+def test_every_gradient_kernel_vs_f64(wk, orc, monkeypatch, impl, B, skip_at):
+    """each matrix-core kernel (WK_GRAD_IMPL, read at wk_create): producer / consumer pairs,
+    tile-parallel teams (two or one per block, the default below 32,768 samples) and one wave
+    per chunk; 8,192 = one chunk per team (the 8-GPU shard's minibatch), 20,011 = several chunks
+    per team with a ragged last chunk, 600 = fewer chunks than teams"""
+    monkeypatch.setenv("WK_GRAD_IMPL", impl)
+    ag = orc.Agent(seed=SEED)
+    eng = wk.Engine(4, seed=SEED)
+    eng.set_weights(ag.params())
+    S, A, L, G, Ad = _batch(B, B + 7 * (skip_at or 0), skip_at)
+    g, cd, ad, sk = eng.minibatch_gradient(S, A, L, G, Ad)
+    og, ocd, oad, osk = ag.train_batch(S, A, L, G, Ad, b_div=B, apply_adam=False)
+    g64, asum, cd64, ad64, sk64 = ref64.train_batch_grad64(ag.params(), S, A, L, G, Ad, B)
+    _check_against_f64(g, og, g64, asum)
+    assert sk == osk == sk64 == (0 if skip_at is None else 1)
+    assert abs(cd - cd64) <= 1e-5 * (abs(cd64) + 1.0) and abs(ad - ad64) <= 1e-5 * (abs(ad64) + 1.0)
+
+
 def _check_against_f64(g, og, g64, asum):
     assert np.isfinite(g).all()
     scale = np.abs(g64).max()
