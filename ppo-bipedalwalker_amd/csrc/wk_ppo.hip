@@ -536,7 +536,12 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
       if (g < ngroups) mine = mine + gv[g];
     x.slab[x.rank][(size_t)buf * SLAB + p] = mine;
   }
-  __syncthreads();  // (workgroup release: every wave's stores have reached the L2)
+  // every storing wave drains its slab stores before the barrier: the flag's system-scope
+  // release below (buffer_wbl2 in thread 0's wave) writes back only what has reached the L2 by
+  // then, and a peer GPU reads this HBM over xGMI (MI355X_MICROARCH.md, inter-workgroup
+  // visibility: the workgroup barrier alone does not wait for other waves' stores)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   const int t = threadIdx.x;
   if (t == 0)
     __hip_atomic_store(x.flag[x.rank] + blockIdx.x, x.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
