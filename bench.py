@@ -214,9 +214,14 @@ def valu_ceiling(lanes_per_walker, walkers):
             "(a wave64 VALU instruction per 4 cycles)")
 
 
-def update_roofline(prof_k, samples_per_minibatch, walkers, horizon, epochs, update_ms, burst_ms):
-    """SURVEY 8(d) update roofline: the gradient kernel (k_ppo_grad_ws, one launch per
-    minibatch) priced at 36,569 flop per sample over its mean duration -- HIP events around a
+GRAD_KERNEL_DESC = {"k_ppo_grad_ws": "producer/consumer waves",
+                    "k_ppo_grad_tp": "tile-parallel teams of four waves"}
+
+
+def update_roofline(prof_k, samples_per_minibatch, walkers, horizon, epochs, update_ms, burst_ms,
+                    kernel):
+    """SURVEY 8(d) update roofline: the gradient kernel (the one the update launches at this
+    minibatch, wk_grad_kernel; one launch per minibatch) priced at 36,569 flop per sample over its mean duration -- HIP events around a
     burst of back-to-back launches (wk_time_gradient): an event pair around every launch of the
     update adds ~4 us of event overhead to a ~35 us kernel -- and the whole update (gradient +
     reduction + Adam over all minibatches) over its measured time"""
@@ -226,7 +231,8 @@ def update_roofline(prof_k, samples_per_minibatch, walkers, horizon, epochs, upd
     n_mb = epochs * (walkers * horizon // samples_per_minibatch)
     upd_flop = epochs * walkers * horizon * FLOP_GRAD_SAMPLE + n_mb * FLOP_ADAM_MINIBATCH
     upd_tf = upd_flop / (update_ms * 1e-3) / 1e12
-    return {"bound": "mfma", "kernel": "k_ppo_grad_ws (producer/consumer v_mfma_f32_16x16x4_f32)",
+    desc = GRAD_KERNEL_DESC.get(kernel, "")
+    return {"bound": "mfma", "kernel": f"{kernel} ({desc + ', ' if desc else ''}v_mfma_f32_16x16x4_f32)",
             "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
             "samples_per_launch": samples_per_minibatch, "flop_per_sample": FLOP_GRAD_SAMPLE,
@@ -317,7 +323,8 @@ def extra_config(wk, torch, args, n, M, M_global, horizon, physics_only=False, m
                 / max(1e-9, prof["physics_ms"] * 1e-3),
                 "ppo_update_ms": upd_ms,
                 "minibatches_per_update": args.epochs * (n * horizon // M),
-                "roofline_update": update_roofline(prof_k, M, n, horizon, args.epochs, upd_ms, burst)}
+                "roofline_update": update_roofline(prof_k, M, n, horizon, args.epochs, upd_ms, burst,
+                                                   eng.grad_kernel(M))}
     finally:
         eng.close()
 
@@ -538,7 +545,8 @@ def main():
         },
         "kernel_ms_one_step": {k: v for k, v in prof_k.items() if k.endswith("_ms")},
         "roofline_update": update_roofline(prof_k, shard.minibatch_local, shard.n_local, T,
-                                           args.epochs, upd_ms_max / args.steps, grad_burst_ms),
+                                           args.epochs, upd_ms_max / args.steps, grad_burst_ms,
+                                           eng.grad_kernel(shard.minibatch_local)),
     }
     if world == 1 and not args.rehearse:
         out["allreduce_1rank"] = allreduce_one_rank(wk, eng, args, T, upd)

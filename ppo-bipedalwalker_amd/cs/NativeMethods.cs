@@ -235,6 +235,7 @@ public static class Wk
     [DllImport(Lib)] public static extern int wk_count_events(IntPtr ctx, int k, ulong[] counts);
     [DllImport(Lib)] public static extern int wk_snapshot(IntPtr ctx, int op);
     [DllImport(Lib)] public static extern int wk_time_gradient(IntPtr ctx, int minibatch, int reps, out double msPerLaunch);
+    [DllImport(Lib)] public static extern int wk_grad_kernel(IntPtr ctx, int minibatch);
 
     public static string LastError(IntPtr ctx) => Marshal.PtrToStringAnsi(wk_last_error(ctx)) ?? "";
 

@@ -1077,6 +1077,11 @@ static int ppo_update_impl(wk_ctx* c, const wk_ppo_args* args);
 // (update 0, epoch 0) of the current trajectory, between one HIP-event pair on the context's
 // stream: the kernel's mean duration without per-launch event overhead (bench.py's update
 // roofline; the launches write only the scratch slabs, no weights change)
+int wk_grad_kernel(wk_ctx* c, int minibatch) {
+  if (!c || minibatch < 0) return WK_ERR_ARG;
+  return wk::grad_impl_for(c->grad_impl, minibatch > 0 ? minibatch : c->cfg.Minibatch);
+}
+
 int wk_time_gradient(wk_ctx* c, int minibatch, int reps, double* ms_per_launch) {
   DevGuard dg_(c);
   if (!c || reps <= 0 || !ms_per_launch) return WK_ERR_ARG;

@@ -40,6 +40,7 @@ EXPORTS = [
     "wk_episode_log_drain", "wk_loss_log_drain", "wk_write_data_file",
     "wk_comm_unique_id", "wk_comm_init", "wk_comm_init_host", "wk_allreduce_test", "wk_profile_enable",
     "wk_profile_get", "wk_profile_reset", "wk_count_events", "wk_snapshot", "wk_time_gradient",
+    "wk_grad_kernel",
     "wk_comm_ipc_handle", "wk_comm_init_ipc",
 ]
 
@@ -234,6 +235,7 @@ def load_library(path=None):
         "wk_allreduce_test": (I, [P, P, I]),
         "wk_comm_init_host": (I, [P, I, I, HOST_ALLREDUCE_FN, P]),
         "wk_time_gradient": (I, [P, I, I, C.POINTER(C.c_double)]),
+        "wk_grad_kernel": (I, [P, I]),
         "wk_comm_ipc_handle": (I, [P, P]),
         "wk_comm_init_ipc": (I, [P, I, I, P]),
         "wk_profile_enable": (I, [P, I]),
@@ -690,6 +692,16 @@ class Engine:
         x = _f32(x).copy()
         self._chk(self.lib.wk_allreduce_test(self.h, _ptr(x), x.size), "wk_allreduce_test")
         return x
+
+    GRAD_KERNELS = {0: "k_ppo_grad_ws", 1: "k_ppo_grad_tp", 2: "k_ppo_grad_tp (one team per block)",
+                    3: "k_ppo_grad_mfma"}
+
+    def grad_kernel(self, minibatch=0):
+        """wk_grad_kernel: the name of the gradient kernel the update launches at this per-GPU
+        minibatch (0 = config Minibatch)"""
+        k = self.lib.wk_grad_kernel(self.h, int(minibatch))
+        self._chk(k if k < 0 else 0, "wk_grad_kernel")
+        return self.GRAD_KERNELS[k]
 
     def time_gradient(self, minibatch=0, reps=64):
         """wk_time_gradient: mean ms of the update's gradient kernel over `reps` back-to-back
