@@ -84,6 +84,28 @@ DEV float row_sum16(float v) {
   return v;
 }
 
+// Block slabs of the ordered reduction, written through to memory (sc1 buffer stores): the
+// kernel-end release then has no dirty slab lines to write back out of the L2, and the
+// reduction reads them from other XCDs anyway (tile-parallel kernel 12.9 -> 12.2 us per launch
+// at 8,192 samples, the reduction unchanged).  -DWK_SLAB_SC1=0: plain stores.
+#ifndef WK_SLAB_SC1
+#define WK_SLAB_SC1 1
+#endif
+struct SlabOut {
+  __amdgpu_buffer_rsrc_t r;
+  f4* p;
+  DEV explicit SlabOut(float* base)
+      : r(__builtin_amdgcn_make_buffer_rsrc(base, 0, SLAB * 4, 0x00020000)), p((f4*)base) {}
+  DEV void put(int i, f4 v) const {  // 16-byte element i
+#if WK_SLAB_SC1
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, i * 16, 0, 16);
+#else
+    p[i] = v;
+#endif
+  }
+};
+
 // Optional phase profile (build with -DWK_GRAD_PROF; scripts/grad_prof.py): wave 0 of each block
 // accumulates s_memtime deltas per phase, summed over blocks into g_grad_prof.
 #ifdef WK_GRAD_PROF
@@ -975,7 +997,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
   }
   __syncthreads();
   // the block fold over the four pair slabs, in pair order
-  f4* out = (f4*)(ga.partial + (size_t)blockIdx.x * SLAB);
+  const SlabOut out(ga.partial + (size_t)blockIdx.x * SLAB);
   constexpr int NV = SLAB / 4, PER = (NV + 512 - 1) / 512;
   f4 sv[PER][PAIRS];
 #pragma unroll
@@ -990,7 +1012,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
     f4 acc = z4;
 #pragma unroll
     for (int w = 0; w < PAIRS; w++) acc = acc + sv[k][w];
-    if (i < NV) out[i] = acc;
+    if (i < NV) out.put(i, acc);
   }
 }
 
@@ -1027,9 +1049,6 @@ template <int TEAMS> struct L {
 };
 }  // namespace tp
 
-#ifndef WK_SLAB_SC1
-#define WK_SLAB_SC1 1
-#endif
 template <int TEAMS>
 __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
   using namespace mf;
@@ -1340,10 +1359,7 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
   }
   __syncthreads();
   {
-    // written through to memory (sc1): the kernel-end release then has no dirty slab lines to
-    // write back out of the L2 (the ordered reduction reads them from another XCD anyway)
-    f4* const out = (f4*)(ga.partial + (size_t)blockIdx.x * SLAB);
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, SLAB * 4, 0x00020000);
+    const SlabOut out(ga.partial + (size_t)blockIdx.x * SLAB);
     constexpr int NV = SLAB / 4, PER = (NV + 256 * TEAMS - 1) / (256 * TEAMS);
     f4 sv[PER][TEAMS];
 #pragma unroll
@@ -1357,13 +1373,7 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
       const int i = tid + k * 256 * TEAMS;
       f4 acc = sv[k][0];
       if (TEAMS == 2) acc = acc + sv[k][TEAMS - 1];
-#if WK_SLAB_SC1
-      typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-      if (i < NV) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc), rsrc, i * 16, 0, 16);
-#else
-      (void)rsrc;
-      if (i < NV) out[i] = acc;
-#endif
+      if (i < NV) out.put(i, acc);
     }
   }
   GP_MARK(9);  // slab
