@@ -164,3 +164,16 @@ def test_ppo_update_config3_vs_oracle(wk, orc):
     _check_against_f64(g, og, g64, asum)
     assert cd == pytest.approx(ocd, rel=1e-3, abs=1e-6)
     assert ad == pytest.approx(oad, rel=1e-3, abs=1e-6)
+
+
+def test_grad_kernel_selection(wk, monkeypatch):
+    """wk_grad_kernel: the tile-parallel kernel below 32,768 samples per launch, the
+    producer / consumer kernel from there; WK_GRAD_IMPL (read at wk_create) overrides"""
+    eng = wk.Engine(256, seed=SEED, Horizon=64, Minibatch=8192)
+    assert eng.grad_kernel() == "k_ppo_grad_tp"
+    assert eng.grad_kernel(32767) == "k_ppo_grad_tp"
+    assert eng.grad_kernel(32768) == "k_ppo_grad_ws"
+    assert eng.grad_kernel(65536) == "k_ppo_grad_ws"
+    monkeypatch.setenv("WK_GRAD_IMPL", "mf")
+    assert wk.Engine(4, seed=SEED).grad_kernel(8192) == "k_ppo_grad_mfma"
+    assert eng.grad_kernel(8192) == "k_ppo_grad_tp"  # per context
