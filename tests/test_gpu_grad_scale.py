@@ -60,7 +60,7 @@ def test_minibatch_gradient_multichunk_vs_oracle(wk, orc, B, skip_at):
 
 
 @pytest.mark.parametrize("impl", ["ws", "tp", "tp1", "mf"])
-@pytest.mark.parametrize("B,skip_at", [(8192, 77), (20011, 20010), (600, None)])
+@pytest.mark.parametrize("B,skip_at", [(8192, 77), (20011, 20010), (600, None), (17, 16), (1, None)])
 def test_every_gradient_kernel_vs_f64(wk, orc, monkeypatch, impl, B, skip_at):
     """each matrix-core kernel (WK_GRAD_IMPL, read at wk_create): producer / consumer pairs,
     tile-parallel teams (two or one per block, the default below 32,768 samples) and one wave
