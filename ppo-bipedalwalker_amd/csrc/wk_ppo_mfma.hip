@@ -850,6 +850,9 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
     if (ga.samples >= 0) return;
 #endif
     // ---- producer totals over the 16 sample lanes of each row ----
+#ifdef WK_GRAD_NOROWSUM  // probe: no row sums (fixed-cost measurement)
+    if (ga.samples < 0)
+#endif
 #pragma unroll
     for (int M = 0; M < 4; M++)
 #pragma unroll
@@ -1012,6 +1015,9 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
     f4 acc = z4;
 #pragma unroll
     for (int w = 0; w < PAIRS; w++) acc = acc + sv[k][w];
+#ifdef WK_GRAD_NOWRITE  // probe: no slab write (fixed-cost measurement)
+    if (ga.samples < 0)
+#endif
     if (i < NV) out.put(i, acc);
   }
 }
