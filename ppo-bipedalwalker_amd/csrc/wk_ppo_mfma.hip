@@ -1037,11 +1037,12 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
 //   backward  dW2[tile w][:] += gz2^T H1                 (16 MFMAs)
 //             gh1 of tile w = W2[:][tile w]^T gz2        (16 MFMAs, B = G2 tile from LDS)
 //             dW1 | db1, dWc1 | dbc1 rows of tile w      (8 MFMAs)
-// 62 MFMAs per wave and chunk, three team barriers, weights in registers straight from the
-// image (no LDS staging).  Every accumulator's k order is the one k_ppo_grad_ws uses; only the
-// z3 / V dots are associated per tile.  A block holds TEAMS teams on separate chunks (two waves
-// per SIMD); the teams' slabs are folded in team order.  Each wave writes its own parameters,
-// so a one-team block needs no fold at all.
+// 62 MFMAs per wave and chunk, three block barriers per chunk (shared by the block's teams),
+// weights in registers straight from the image (no LDS staging).  Every accumulator's k order
+// is the one k_ppo_grad_ws uses; only the z3 / V dots are associated per tile.  A block holds
+// TEAMS teams on separate chunks (two waves per SIMD).  At the end each wave writes its own
+// parameters into its team's slab in LDS and the block writes the teams' sum (team order) as
+// its partial slab.
 namespace tp {
 enum : int {
   RT = 68, T68 = 16 * RT, RSX = 20, TSX = 16 * RSX, RP = 80,  // P: [wave 4][d 5][16 samples]
