@@ -379,6 +379,8 @@ def main():
         dist.init_process_group("gloo")  # control plane only; gradients go over RCCL
     if args.rehearse:
         local = 0
+    elif torch.cuda.device_count() == 1 and local > 0:
+        local = 0  # a launcher that shows each rank only its own GPU (HIP_VISIBLE_DEVICES)
     torch.cuda.set_device(local)
     weak = args.walkers > 0
     if weak:
