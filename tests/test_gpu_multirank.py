@@ -1,4 +1,4 @@
-"""GPU, two processes sharing GPU 0: libwk's multi-rank minibatch sequence.
+"""GPU, two (and three) processes sharing GPU 0: libwk's multi-rank minibatch sequence.
 
 RCCL refuses two ranks on one device, so the ranks' all-reduce goes through
 wk_comm_init_host (the same sequence: ordered block reduction -> all-reduce of the 6,153-float
@@ -50,11 +50,11 @@ def _adam_t1(w, g, alpha=np.float32(0.001), beta1=0.9, beta2=0.999, eps=np.float
     return w - ((mh / den) * alpha), m, v
 
 
-def _run_two_ranks(out, mode):
+def _run_two_ranks(out, mode, n=2):
     port = _free_port()
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0",
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK="0",
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen(
             ["timeout", "-k", "10", "240", sys.executable,
@@ -63,7 +63,7 @@ def _run_two_ranks(out, mode):
     outs = [p.communicate()[0] for p in procs]
     for p, o in zip(procs, outs):
         assert p.returncode == 0, o[-3000:]
-    return [np.load(out / f"rank{r}.npz") for r in range(2)]
+    return [np.load(out / f"rank{r}.npz") for r in range(n)]
 
 
 @pytest.fixture(scope="module")
@@ -101,6 +101,26 @@ def test_ipc_exchange_equals_host_allreduce(two_rank_runs):
         for k in ("w1", "m1", "v1", "w2", "w3", "m3", "v3", "state"):
             np.testing.assert_array_equal(h[k], i[k], err_msg=k)
         assert float(h["cd"]) == float(i["cd"]) and float(h["ad"]) == float(i["ad"])
+
+
+def test_three_ranks_ipc_rank_order_sum(tmp_path):
+    """three processes (an odd rank count): the IPC exchange sums the ranks' local slabs in rank
+    order, ((g0 + g1) + g2) in float32, and every replica applies the same Adam step"""
+    rs = _run_two_ranks(tmp_path, "ipc", n=3)
+    for r in rs:
+        assert r["same_traj"] and r["same_state"]
+    g_sum = (rs[0]["g_local"] + rs[1]["g_local"]) + rs[2]["g_local"]
+    w_ref, m_ref, v_ref = _adam_t1(rs[0]["w0"], g_sum)
+    cd_ref = (np.float32(rs[0]["cd_l"]) + np.float32(rs[1]["cd_l"])) + np.float32(rs[2]["cd_l"])
+    for r in rs:
+        np.testing.assert_array_equal(r["w1"], w_ref)
+        np.testing.assert_array_equal(r["m1"], m_ref)
+        np.testing.assert_array_equal(r["v1"], v_ref)
+        assert float(r["cd"]) == cd_ref
+    for k in ("w2", "w3", "m3", "v3"):
+        np.testing.assert_array_equal(rs[0][k], rs[1][k], err_msg=k)
+        np.testing.assert_array_equal(rs[0][k], rs[2][k], err_msg=k)
+    assert int(rs[2]["t3"]) == 2 + 2 * 3 * 4
 
 
 def test_failing_host_allreduce_is_reported(wk):
