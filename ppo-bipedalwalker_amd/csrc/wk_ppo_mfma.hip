@@ -582,11 +582,13 @@ enum : int {
   RT = 68, T68 = 16 * RT, RSX = 20, TSX = 16 * RSX,
   O_SX = 0, O_H1 = TSX, O_G2 = O_H1 + T68, O_GC1 = O_G2 + T68, TB = O_GC1 + T68,
   PAIRS = 4,
+  PV = 101,  // the producer's per-lane partials summed over sample lanes at the end
   LOOP_FLOATS = mf::WEND + PAIRS * 2 * TB,
   LDS_FLOATS = LOOP_FLOATS > PAIRS * SLAB ? LOOP_FLOATS : PAIRS * SLAB
 };
 static_assert(LOOP_FLOATS * 4 <= 160 * 1024, "fits the CU's LDS");
 static_assert(TB % 4 == 0 && T68 % 4 == 0 && TSX % 4 == 0, "16-byte aligned tiles");
+static_assert(PAIRS * PV * 64 <= LDS_FLOATS, "the producers' partials fit");
 }  // namespace ws
 
 __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga) {
@@ -672,6 +674,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
   float* const pt = lds + WEND + pair * 2 * TB;  // this pair's two tile buffers
   const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
 
+  f4 a2[4][4], a1[4], a1c[4];  // the consumer's accumulators (written into its slab at the end)
   if (producer) {
     // ---------------- producer ----------------
     // (the producer's dependent chain sets the pace: the SIMD's arbiter serves it first, the
@@ -849,49 +852,27 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
 #ifdef WK_GRAD_NOEPI  // probe: no epilogue
     if (ga.samples >= 0) return;
 #endif
-    // ---- producer totals over the 16 sample lanes of each row ----
-#ifdef WK_GRAD_NOROWSUM  // probe: no row sums (fixed-cost measurement)
-    if (ga.samples < 0)
-#endif
+    __syncthreads();  // every wave is done with the weights and tiles
+    // ---- the producer's per-lane partials, raw, to R[pair][v][lane]: the whole block forms
+    // their sums over the 16 sample lanes of each row below (v order: db2, dWc2, dW3 by
+    // (d, M, r), then db3, dbc2 and the three diagnostics) ----
+    float* const R = lds + pair * (PV * 64) + lane;
 #pragma unroll
     for (int M = 0; M < 4; M++)
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        db2[M][r] = row_sum16(db2[M][r]);
-        awc2[M][r] = row_sum16(awc2[M][r]);
+        R[(4 * M + r) * 64] = db2[M][r];
+        R[(16 + 4 * M + r) * 64] = awc2[M][r];
 #pragma unroll
-        for (int d = 0; d < 4; d++) aw3[d][M][r] = row_sum16(aw3[d][M][r]);
+        for (int d = 0; d < 4; d++) R[(32 + 16 * d + 4 * M + r) * 64] = aw3[d][M][r];
       }
-    db3 = row_sum16(db3);
-    dbc2 = row_sum16(dbc2);
-    diagC = row_sum16(diagC);
-    diagA = row_sum16(diagA);
-    skipped = row_sum16(skipped);
-    __syncthreads();  // every wave is done with the weights and tiles
-    float* slab = lds + pair * SLAB;
-    if (lane < SLAB - (NPARAM + 3)) slab[NPARAM + 3 + lane] = 0.0f;  // (the pads)
-    if (n == 0) {
-#pragma unroll
-      for (int M = 0; M < 4; M++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int j = 16 * M + 4 * g + r;
-          slab[OFF_A_B2 + j] = db2[M][r];
-          slab[OFF_C_W2 + j] = awc2[M][r];
-#pragma unroll
-          for (int d = 0; d < 4; d++) slab[OFF_A_W3 + d * 64 + j] = aw3[d][M][r];
-        }
-      slab[OFF_A_B3 + g] = db3;
-      if (g == 0) {
-        slab[OFF_C_B2] = dbc2;
-        slab[NPARAM] = diagC;
-        slab[NPARAM + 1] = diagA;
-        slab[NPARAM + 2] = skipped;
-      }
-    }
+    R[96 * 64] = db3;
+    R[97 * 64] = dbc2;
+    R[98 * 64] = diagC;
+    R[99 * 64] = diagA;
+    R[100 * 64] = skipped;
   } else {
     // ---------------- consumer ----------------
-    f4 a2[4][4], a1[4], a1c[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       a1[i] = z4; a1c[i] = z4;
@@ -981,6 +962,39 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
     if (ga.samples >= 0) return;
 #endif
     __syncthreads();  // (matches the producer's: weights and tiles are free)
+  }
+  __syncthreads();  // the producers' partials are in R
+  // ---- row sums: item (pair, v, g) = the 16 lanes of row g of partial v, four 16-byte reads
+  // and a fixed tree; at most four items per thread ----
+  constexpr int NITEM = PAIRS * PV * 4, KI = (NITEM + 511) / 512;
+  float rsum[KI];
+  int rdst[KI];
+#pragma unroll
+  for (int k = 0; k < KI; k++) {
+    const int i = tid + k * 512;
+    rdst[k] = -1;
+    rsum[k] = 0.0f;
+    if (i < NITEM) {
+      const int p = i / (PV * 4), v = (i / 4) % PV, gg = i & 3;
+      const f4* q = (const f4*)(lds + (p * PV + v) * 64 + 16 * gg);
+      const f4 t = (q[0] + q[1]) + (q[2] + q[3]);
+      rsum[k] = (t[0] + t[1]) + (t[2] + t[3]);
+      int dst;
+      if (v < 16) dst = OFF_A_B2 + 16 * (v >> 2) + 4 * gg + (v & 3);
+      else if (v < 32) dst = OFF_C_W2 + 16 * ((v - 16) >> 2) + 4 * gg + (v & 3);
+      else if (v < 96) dst = OFF_A_W3 + ((v - 32) >> 4) * 64 + 16 * (((v - 32) >> 2) & 3) + 4 * gg + (v & 3);
+      else if (v == 96) dst = OFF_A_B3 + gg;
+      else dst = gg == 0 ? (v == 97 ? OFF_C_B2 : NPARAM + (v - 98)) : -1;  // (sample terms: row 0)
+      rdst[k] = dst < 0 ? -1 : p * SLAB + dst;
+    }
+  }
+  __syncthreads();  // R is read: the pair slabs may overwrite it
+#pragma unroll
+  for (int k = 0; k < KI; k++)
+    if (rdst[k] >= 0) lds[rdst[k]] = rsum[k];
+  if (producer) {
+    if (lane < SLAB - (NPARAM + 3)) lds[pair * SLAB + NPARAM + 3 + lane] = 0.0f;  // (the pads)
+  } else {
     float* slab = lds + pair * SLAB;
 #pragma unroll
     for (int Mj = 0; Mj < 4; Mj++)
