@@ -88,7 +88,7 @@ struct wk_ctx {
   wk_host_allreduce_fn host_ar = nullptr;  // wk_comm_init_host: a caller-supplied all-reduce
   void* host_ar_user = nullptr;
   std::vector<float> host_ar_buf;
-  // wk_comm_init_ipc: the one-shot exchange over peer-mapped memory (k_xch_adam)
+  // wk_comm_init_ipc: the one-shot exchange over peer-mapped memory (k_reduce_xch_adam)
   void* xch = nullptr;                 // this rank's exchange region (exported by IPC handle)
   std::vector<void*> xch_peers;        // peers' regions, opened from their handles
   wk::XchArgs xa{};                    // slab / flag pointers of every rank
