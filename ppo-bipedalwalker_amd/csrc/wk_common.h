@@ -146,6 +146,7 @@ struct EnvParams {
   int env_offset;
   int lanes;            // lanes per walker in the env-step kernel (1, 2 or 16)
   int rough;            // Hyperparameters.RoughFloor: 10 static floor segments
+  int sparse;           // quad mapping with eight walkers per wave (k_env_side, n <= 8,192)
 };
 
 }  // namespace wk

@@ -1163,10 +1163,16 @@ void k_env_side(EnvParams P, StepArgs A) {
   const int half = Q == 2 ? (tid >> 1) & 1 : 0;
   constexpr int SH = Q == 2 ? 2 : 1;  // log2 lanes per walker
   const int n = P.n_env;
+  // sparse quad mapping (P.sparse: at most 8,192 walkers, so one wave per SIMD holds them
+  // all even at eight walkers per wave): eight walkers per wave in lanes 0..31, lanes 32..63
+  // replay them (same walker, same branches, never store), so a wave's divergent branches are
+  // the union over eight walkers instead of sixteen
+  const bool SPARSE = Q == 2 && P.sparse;
+  const int eraw = SPARSE ? ((tid >> 6) << 3) + ((tid & 31) >> 2) : (tid >> SH);
   // a partial last wave keeps every lane (the policy's MFMAs need the whole wave):
   // out-of-range lanes replay walker n-1 and never store
-  const bool active = (tid >> SH) < n;
-  const int e = active ? (tid >> SH) : n - 1;
+  const bool active = eraw < n && !(SPARSE && (tid & 32));
+  const int e = eraw < n ? eraw : n - 1;
   const bool leader = side == 0 && half == 0 && active;
   __shared__ float pol_lds[POLICY ? (SIDE_BLOCK / 64) * 768 : 1];
   __shared__ float wz_lds[POLICY ? mf::WEND : 1];  // operand-order weights (41 KB, 2 blocks/CU)
@@ -1174,11 +1180,12 @@ void k_env_side(EnvParams P, StepArgs A) {
   // [draw][walker of block]; the walker's lanes write the same values and read only its column
   constexpr int WPB = SIDE_BLOCK >> SH;
   __shared__ float ter_lds[ROUGH ? 11 * WPB : 1];
-  const float* const ter = ter_lds + (threadIdx.x >> SH);
+  const int wib = SPARSE ? ((threadIdx.x >> 6) << 3) + ((threadIdx.x & 31) >> 2) : (threadIdx.x >> SH);
+  const float* const ter = ter_lds + wib;
   if constexpr (ROUGH) {
 #pragma unroll 1
     for (int i = 0; i < 11; i++)
-      ter_lds[i * WPB + (threadIdx.x >> SH)] = 800.0f + (float)terrain_draw(P.seed, (uint32_t)(P.env_offset + e), i);
+      ter_lds[i * WPB + wib] = 800.0f + (float)terrain_draw(P.seed, (uint32_t)(P.env_offset + e), i);
   }
   if (POLICY) {
     for (int i = threadIdx.x; i < mf::WEND / 4; i += SIDE_BLOCK)
@@ -1411,7 +1418,8 @@ static void launch_lanes(int mode, const EnvParams& P, const StepArgs& A, hipStr
 #if WK_PART(1) || WK_PART(5)
 template <int Q, bool ROUGH>
 static void launch_side(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
-  dim3 blk(SIDE_BLOCK), grd((unsigned)(((size_t)P.n_env * 2 * Q + SIDE_BLOCK - 1) / SIDE_BLOCK));
+  const size_t lanes = (size_t)P.n_env * 2 * Q * (Q == 2 && P.sparse ? 2 : 1);
+  dim3 blk(SIDE_BLOCK), grd((unsigned)((lanes + SIDE_BLOCK - 1) / SIDE_BLOCK));
   switch (mode) {
     case 0: hipLaunchKernelGGL((k_env_side<false, false, false, Q, ROUGH>), grd, blk, 0, s, P, A); break;
     case 1: hipLaunchKernelGGL((k_env_side<false, false, true, Q, ROUGH>), grd, blk, 0, s, P, A); break;
