@@ -329,13 +329,16 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   // pairs run unsplit in every mapping, the leg-leg pairs keep the pair / quad split.
   P.lanes = c.LanesPerWalker ? c.LanesPerWalker : (n_env <= 16384 ? 4 : 2);
   P.rough = c.RoughFloor ? 1 : 0;
-  // the quad mapping at eight walkers per wave (lanes 32..63 replay lanes 0..31) while one wave
-  // per SIMD still holds every walker (n <= 8,192 on 1,024 SIMDs): each wave's divergent
-  // branches are the union over eight walkers instead of sixteen -- rollout 5.72 -> 5.52 ms per
-  // 16 env-steps at 8,192 walkers, physics only 5.95 -> 5.62 (WK_QUAD_SPARSE=0 turns it off)
+  // the quad mapping with fewer walkers per wave (the other lanes replay them) while one wave
+  // per SIMD still holds every walker (1,024 SIMDs): each wave's divergent branches are the
+  // union over fewer walkers -- rollout 5.72 -> 5.52 ms per 16 env-steps at 8,192 walkers
+  // (eight per wave), physics only 5.95 -> 5.62.  WK_QUAD_SPARSE=0: always sixteen
   {
     const char* sp = getenv("WK_QUAD_SPARSE");
-    P.sparse = (P.lanes == 4 && n_env <= 8192 && !(sp && sp[0] == '0')) ? 1 : 0;
+    int wpw = 16;
+    if (!(sp && sp[0] == '0'))
+      while (wpw > 1 && (size_t)n_env <= (size_t)512 * wpw) wpw >>= 1;  // n / (wpw / 2) <= 1,024 waves
+    P.wpw = wpw;
   }
   const float PI_F = 3.14159265358979323846f;
   x->lp_const = -logf(P.std_) - logf(sqrtf(2.0f * PI_F));

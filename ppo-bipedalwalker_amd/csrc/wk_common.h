@@ -146,7 +146,7 @@ struct EnvParams {
   int env_offset;
   int lanes;            // lanes per walker in the env-step kernel (1, 2 or 16)
   int rough;            // Hyperparameters.RoughFloor: 10 static floor segments
-  int sparse;           // quad mapping with eight walkers per wave (k_env_side, n <= 8,192)
+  int wpw;              // quad mapping: walkers per wave (16; fewer, down to 1, at small n)
 };
 
 }  // namespace wk

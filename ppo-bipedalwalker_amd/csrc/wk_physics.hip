@@ -1163,15 +1163,15 @@ void k_env_side(EnvParams P, StepArgs A) {
   const int half = Q == 2 ? (tid >> 1) & 1 : 0;
   constexpr int SH = Q == 2 ? 2 : 1;  // log2 lanes per walker
   const int n = P.n_env;
-  // sparse quad mapping (P.sparse: at most 8,192 walkers, so one wave per SIMD holds them
-  // all even at eight walkers per wave): eight walkers per wave in lanes 0..31, lanes 32..63
-  // replay them (same walker, same branches, never store), so a wave's divergent branches are
-  // the union over eight walkers instead of sixteen
-  const bool SPARSE = Q == 2 && P.sparse;
-  const int eraw = SPARSE ? ((tid >> 6) << 3) + ((tid & 31) >> 2) : (tid >> SH);
+  // sparse quad mapping (P.wpw < 16 walkers per wave, chosen so that one wave per SIMD still
+  // holds every walker): the wave's first 4 wpw lanes hold wpw walkers, the other lanes replay
+  // them (same walker, same branches, never store), so a wave's divergent branches are the
+  // union over wpw walkers instead of sixteen
+  const int wpw = Q == 2 ? P.wpw : 64 >> SH;  // (a power of two)
+  const int eraw = ((tid >> 6) * wpw) + ((tid & ((wpw << SH) - 1)) >> SH);
   // a partial last wave keeps every lane (the policy's MFMAs need the whole wave):
   // out-of-range lanes replay walker n-1 and never store
-  const bool active = eraw < n && !(SPARSE && (tid & 32));
+  const bool active = eraw < n && (tid & 63) < (wpw << SH);
   const int e = eraw < n ? eraw : n - 1;
   const bool leader = side == 0 && half == 0 && active;
   __shared__ float pol_lds[POLICY ? (SIDE_BLOCK / 64) * 768 : 1];
@@ -1180,7 +1180,7 @@ void k_env_side(EnvParams P, StepArgs A) {
   // [draw][walker of block]; the walker's lanes write the same values and read only its column
   constexpr int WPB = SIDE_BLOCK >> SH;
   __shared__ float ter_lds[ROUGH ? 11 * WPB : 1];
-  const int wib = SPARSE ? ((threadIdx.x >> 6) << 3) + ((threadIdx.x & 31) >> 2) : (threadIdx.x >> SH);
+  const int wib = ((threadIdx.x >> 6) * wpw) + ((threadIdx.x & ((wpw << SH) - 1)) >> SH);
   const float* const ter = ter_lds + wib;
   if constexpr (ROUGH) {
 #pragma unroll 1
@@ -1418,7 +1418,7 @@ static void launch_lanes(int mode, const EnvParams& P, const StepArgs& A, hipStr
 #if WK_PART(1) || WK_PART(5)
 template <int Q, bool ROUGH>
 static void launch_side(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
-  const size_t lanes = (size_t)P.n_env * 2 * Q * (Q == 2 && P.sparse ? 2 : 1);
+  const size_t lanes = Q == 2 ? ((size_t)P.n_env + P.wpw - 1) / P.wpw * 64 : (size_t)P.n_env * 2;
   dim3 blk(SIDE_BLOCK), grd((unsigned)((lanes + SIDE_BLOCK - 1) / SIDE_BLOCK));
   switch (mode) {
     case 0: hipLaunchKernelGGL((k_env_side<false, false, false, Q, ROUGH>), grd, blk, 0, s, P, A); break;
