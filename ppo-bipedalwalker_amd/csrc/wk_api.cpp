@@ -338,6 +338,10 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
     int wpw = 16;
     if (!(sp && sp[0] == '0'))
       while (wpw > 1 && (size_t)n_env <= (size_t)512 * wpw) wpw >>= 1;  // n / (wpw / 2) <= 1,024 waves
+    if (const char* f = getenv("WK_QUAD_WPW")) {  // (experiments: a forced power of two)
+      const int v = atoi(f);
+      if (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) wpw = v;
+    }
     P.wpw = wpw;
   }
   const float PI_F = 3.14159265358979323846f;
