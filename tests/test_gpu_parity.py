@@ -445,3 +445,37 @@ def test_collective_path_matches_single_gpu_path(wk):
         np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
     assert out[0][2] == out[1][2] and out[0][3] == out[1][3]
     np.testing.assert_array_equal(a.get_state(), b.get_state())
+
+
+@pytest.mark.parametrize("n", [1500, 5000, 8193])
+def test_quad_walkers_per_wave_ragged(wk, orc, n):
+    """the quad mapping's walkers per wave follow n (2 at 1,500, 8 at 5,000, 16 at 8,193; the
+    last wave partial in each): physics bit-exact against the oracle"""
+    k = 12
+    eng = wk.Engine(n, seed=SEED, RandomizeStart=1, RandomizeMaterial=1, LanesPerWalker=4)
+    envs, _, _ = oracle_envs(orc, eng, n)
+    acts = np.random.default_rng(n).uniform(-1.2, 1.2, (k, n, 4)).astype(F)
+    obs, rew, done, fault = eng.step(acts, k=k)
+    for i, e in enumerate(envs):
+        for t in range(k):
+            o, r, d = e.step(acts[t, i])
+            assert r == rew[t, i] and d == done[t, i], (i, t)
+            np.testing.assert_array_equal(o, obs[t, i])
+    np.testing.assert_array_equal(eng.get_state(), np.stack([e.dump() for e in envs]))
+    assert not fault.any()
+
+
+def test_quad_sparse_equals_dense(wk, monkeypatch):
+    """at the 8-GPU shard (8,192 walkers) the sparse quad mapping (eight walkers per wave, the
+    other lanes replaying them) and the dense one (sixteen per wave, WK_QUAD_SPARSE=0) give the
+    same policy rollout bit for bit: trajectory, returns and final state"""
+    n, T = 8192, 24
+    eng = wk.Engine(n, seed=SEED, RandomizeStart=1, RandomizeMaterial=1, Horizon=T)
+    monkeypatch.setenv("WK_QUAD_SPARSE", "0")
+    dense = wk.Engine(n, seed=SEED, RandomizeStart=1, RandomizeMaterial=1, Horizon=T)
+    for x in (eng, dense):
+        x.rollout(T)
+    a, b = eng.get_trajectory(T), dense.get_trajectory(T)
+    for key in a:
+        np.testing.assert_array_equal(a[key], b[key], err_msg=key)
+    np.testing.assert_array_equal(eng.get_state(), dense.get_state())
