@@ -215,7 +215,8 @@ def valu_ceiling(lanes_per_walker, walkers):
 
 
 GRAD_KERNEL_DESC = {"k_ppo_grad_ws": "producer/consumer waves",
-                    "k_ppo_grad_tp": "tile-parallel teams of four waves"}
+                    "k_ppo_grad_tp": "tile-parallel teams of four waves, two per block",
+                    "k_ppo_grad_tp1": "tile-parallel teams of four waves, one per block"}
 
 
 def update_roofline(prof_k, samples_per_minibatch, walkers, horizon, epochs, update_ms, burst_ms,

@@ -429,7 +429,8 @@ int wk_time_gradient(wk_ctx* ctx, int minibatch, int reps, double* ms_per_launch
 /* Which matrix-core gradient kernel the update launches for a per-GPU minibatch of `minibatch`
  * samples (0 = config Minibatch): 0 producer / consumer waves (k_ppo_grad_ws), 1 tile-parallel
  * teams (k_ppo_grad_tp, two per block), 2 the same with one team per block, 3 one wave per chunk
- * (k_ppo_grad_mfma).  By size unless WK_GRAD_IMPL = ws / tp / tp1 / mf was set at wk_create. */
+ * (k_ppo_grad_mfma).  By size (tp1 up to 4,096 samples, tp below 32,768, ws from there) unless
+ * WK_GRAD_IMPL = ws / tp / tp1 / mf was set at wk_create. */
 int wk_grad_kernel(wk_ctx* ctx, int minibatch);
 
 #ifdef __cplusplus

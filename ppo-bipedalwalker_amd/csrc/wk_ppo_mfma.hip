@@ -1438,7 +1438,10 @@ int grad_impl_env() {
 }
 int grad_impl_for(int impl, int samples) {
   if (impl != GI_AUTO) return impl;
-  return samples < 32768 ? GI_TP2 : GI_WS;
+  // one team per block up to 256 chunks (one chunk per block on every CU: 7.6 vs 9.5 us at
+  // 4,096 samples), two from there (8,192: 10.5 vs 11.3 us), the producer / consumer kernel
+  // from 32,768
+  return samples <= 4096 ? GI_TP1 : samples < 32768 ? GI_TP2 : GI_WS;
 }
 hipError_t configure_mfma_kernels() {
   hipError_t e = hipFuncSetAttribute((const void*)k_ppo_grad_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,

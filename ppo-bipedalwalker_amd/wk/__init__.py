@@ -693,7 +693,7 @@ class Engine:
         self._chk(self.lib.wk_allreduce_test(self.h, _ptr(x), x.size), "wk_allreduce_test")
         return x
 
-    GRAD_KERNELS = {0: "k_ppo_grad_ws", 1: "k_ppo_grad_tp", 2: "k_ppo_grad_tp (one team per block)",
+    GRAD_KERNELS = {0: "k_ppo_grad_ws", 1: "k_ppo_grad_tp", 2: "k_ppo_grad_tp1",
                     3: "k_ppo_grad_mfma"}
 
     def grad_kernel(self, minibatch=0):

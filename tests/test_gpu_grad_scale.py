@@ -167,10 +167,13 @@ def test_ppo_update_config3_vs_oracle(wk, orc):
 
 
 def test_grad_kernel_selection(wk, monkeypatch):
-    """wk_grad_kernel: the tile-parallel kernel below 32,768 samples per launch, the
-    producer / consumer kernel from there; WK_GRAD_IMPL (read at wk_create) overrides"""
+    """wk_grad_kernel: the tile-parallel kernel below 32,768 samples per launch (one team per
+    block up to 4,096), the producer / consumer kernel from there; WK_GRAD_IMPL (read at
+    wk_create) overrides"""
     eng = wk.Engine(256, seed=SEED, Horizon=64, Minibatch=8192)
     assert eng.grad_kernel() == "k_ppo_grad_tp"
+    assert eng.grad_kernel(4096) == "k_ppo_grad_tp1"
+    assert eng.grad_kernel(4097) == "k_ppo_grad_tp"
     assert eng.grad_kernel(32767) == "k_ppo_grad_tp"
     assert eng.grad_kernel(32768) == "k_ppo_grad_ws"
     assert eng.grad_kernel(65536) == "k_ppo_grad_ws"
