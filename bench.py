@@ -374,6 +374,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
 
+    import numpy as np
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -408,7 +409,15 @@ def main():
             return out
         try:
             eng.comm_init_ipc(rank, world, allgather)
-            ok = 1
+            # one test round on exact small integers: every rank must see the sum of all
+            # ranks' values (a mapping that cannot be read, or a peer that never publishes,
+            # falls back to RCCL here rather than stalling the timed run)
+            base = (np.arange(wk.NPARAM) % 97).astype(np.float32)
+            got = eng.allreduce_test(base + np.float32(rank + 1))
+            want = base * np.float32(world) + np.float32(world * (world + 1) // 2)
+            ok = 1 if np.array_equal(got, want) else 0
+            if not ok:
+                print(f"rank {rank}: IPC exchange test gave wrong sums; using RCCL", file=sys.stderr)
         except wk.WkError as ex:  # e.g. no peer access between the devices
             print(f"rank {rank}: IPC exchange unavailable ({ex}); using RCCL", file=sys.stderr)
             ok = 0

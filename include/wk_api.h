@@ -369,7 +369,10 @@ int wk_write_data_file(const char* path, const float* total_rewards, int64_t n_r
 /* multi-GPU: RCCL communicator over the ranks' contexts (one per GPU) */
 int wk_comm_unique_id(uint8_t* id /* 128 bytes */);
 int wk_comm_init(wk_ctx* ctx, int rank, int nranks, const uint8_t* unique_id);
-int wk_allreduce_test(wk_ctx* ctx, float* host_buf, int n); /* sum in place (tests) */
+/* sum of host_buf over the ranks, in place, through the context's exchange: RCCL, or with
+ * wk_comm_init_ipc one round of the IPC exchange (n <= 6,152 floats; ranks summed in rank order;
+ * WK_ERR_COMM when a peer never publishes) -- tests, and bench.py's check of a fresh IPC mapping */
+int wk_allreduce_test(wk_ctx* ctx, float* host_buf, int n);
 /* The same minibatch sequence with a caller-supplied all-reduce instead of RCCL: after the
  * ordered reduction each minibatch's slab (gradient + diagnostics, n floats) is copied to the
  * host, fn must replace it in place with the sum over ranks (return 0), and it is copied back

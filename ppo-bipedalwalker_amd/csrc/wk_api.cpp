@@ -1348,6 +1348,28 @@ int wk_comm_init_ipc(wk_ctx* c, int rank, int nranks, const uint8_t* handles) {
 int wk_allreduce_test(wk_ctx* c, float* host_buf, int n) {
   DevGuard dg_(c);
   if (!c || !host_buf || n <= 0) return WK_ERR_ARG;
+  if (c->ipc) {  // one round of the IPC exchange (k_reduce_xch_adam without Adam) on this slab
+    if (n > wk::SLAB) { SETERR(c, "the IPC exchange test takes at most %d floats", (int)wk::SLAB); return WK_ERR_ARG; }
+    if (ensure(c, &c->scratch, &c->scratch_bytes, sizeof(float) * 2 * wk::SLAB)) return WK_ERR_HIP;
+    float* in = (float*)c->scratch;
+    float* out = in + wk::SLAB;
+    HIPCHK(c, hipMemsetAsync(in, 0, sizeof(float) * wk::SLAB, c->stream));
+    HIPCHK(c, hipMemcpyAsync(in, host_buf, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+    wk::XchArgs x = c->xa;
+    x.partial = in;
+    x.nblocks = 1;
+    x.grad_out = out;
+    x.seq = ++c->xch_seq;
+    x.err = c->xch_err;
+    x.a = wk::AdamArgs{};
+    HIPCHK(c, wk::launch_reduce_xch_adam(x, c->stream));
+    HIPCHK(c, hipMemcpyAsync(host_buf, out, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    uint32_t err = 0;
+    HIPCHK(c, hipMemcpy(&err, c->xch_err, sizeof err, hipMemcpyDeviceToHost));
+    if (err) { SETERR(c, "IPC exchange: a peer never published (timeout)"); return WK_ERR_COMM; }
+    return WK_OK;
+  }
   if (ensure(c, &c->scratch, &c->scratch_bytes, sizeof(float) * n)) return WK_ERR_HIP;
   HIPCHK(c, hipMemcpyAsync(c->scratch, host_buf, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
   if (c->comm && c->nranks > 1) {

@@ -504,7 +504,7 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
   const int q = blockIdx.x * QB + qi;
   const int ngroups = (x.nblocks + RG - 1) / RG;
   const int p = 4 * q + gi;  // (gi < 4) this thread's parameter
-  const bool adam_lane = gi < 4 && p < NPARAM;
+  const bool adam_lane = gi < 4 && p < NPARAM && x.a.W != nullptr;  // (no W: exchange only)
   float m0 = 0.0f, v0 = 0.0f, w0 = 0.0f;
   if (adam_lane) { m0 = x.a.m[p]; v0 = x.a.v[p]; w0 = x.a.W[p]; }
   float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);

@@ -39,6 +39,11 @@ if mode == "ipc":
         dist.all_gather_object(out, b)
         return out
     eng.comm_init_ipc(rank, world, allgather)
+    # one round of the exchange on exact small integers (bench.py's check of a fresh mapping)
+    base = (np.arange(wk.NPARAM) % 97).astype(np.float32)
+    ar_test = eng.allreduce_test(base + np.float32(rank + 1))
+    ar_want = base * np.float32(world) + np.float32(world * (world + 1) // 2)
+    assert np.array_equal(ar_test, ar_want), "IPC exchange test round"
 else:
     eng.comm_init_host(rank, world, allreduce)
 w0 = eng.get_weights()
