@@ -91,13 +91,16 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="processes of the all-cores CPU baseline (0: every CPU the process may use)")
     p.add_argument("--rehearse", action="store_true",
-                   help="multi-rank rehearsal on ONE GPU: every rank on device 0, gradients "
-                        "all-reduced on the host over gloo (wk_comm_init_host) instead of RCCL "
-                        "-- exercises the N > 1 code path; not a performance number")
+                   help="multi-rank rehearsal on ONE GPU: every rank on device 0, the exchange "
+                        "either IPC (--exchange ipc, the default) or the host all-reduce over "
+                        "gloo (wk_comm_init_host; RCCL refuses two ranks on one device) -- "
+                        "exercises the N > 1 code path; not a performance number")
     p.add_argument("--exchange", choices=("rccl", "ipc"), default="ipc",
                    help="N > 1 minibatch gradient exchange: the one-shot exchange over IPC-mapped "
                         "peer memory fused with the ordered reduction and Adam (wk_comm_init_ipc; "
-                        "falls back to RCCL if the mapping fails), or the RCCL all-reduce")
+                        "checked bit for bit against a rank-order reference before timing, and "
+                        "RCCL on every rank if the mapping, the test round or the check fails), "
+                        "or the RCCL all-reduce")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_physics.json"))
     return p.parse_args()
 
@@ -203,10 +206,69 @@ def cpu_baseline(args):
 
 
 # ---------------------------------------------------------------- GPU -------------------
-def valu_ceiling(lanes_per_walker, walkers):
-    """the non-FMA VALU ceiling of a rollout launch: 2+ waves per SIMD -> 78.6 T; else one
-    wave per SIMD on the share of SIMDs that hold one (MI355X_MICROARCH.md issue-cost row)"""
-    waves = -(-lanes_per_walker * walkers // 64)
+GRAD_KERNEL_DESC = {"k_ppo_grad_ws": "producer/consumer waves",
+                    "k_ppo_grad_tp": "tile-parallel teams of four waves, two per block",
+                    "k_ppo_grad_tp1": "tile-parallel teams of four waves, one per block"}
+
+
+def update_roofline(prof_k, samples_per_minibatch, walkers, horizon, epochs, update_ms, burst_ms,
+                    burst_ev_ms, kernel, exchange="none"):
+    """SURVEY 8(d) update roofline: the gradient kernel the update launches at this minibatch
+    (wk_grad_kernel; one launch per minibatch) priced at 36,569 flop per sample over its mean
+    duration INSIDE a real update: the per-launch HIP-event mean of one untimed
+    update with an event pair around every launch (profile level 2), minus the per-launch event
+    overhead measured on the same kernel (a burst of back-to-back launches timed with an event
+    pair around every launch, minus the same burst timed by one pair) -- and the whole update
+    (gradient + reduction + exchange + Adam over all minibatches) over its measured time"""
+    launches = max(1, prof_k.get("grad_launches", 0))
+    ev_mean_us = prof_k["grad_ms"] / launches * 1e3
+    overhead_us = max(0.0, (burst_ev_ms - burst_ms) * 1e3)
+    grad_us = ev_mean_us - overhead_us
+    achieved = FLOP_GRAD_SAMPLE * samples_per_minibatch / (grad_us * 1e-6) / 1e12
+    n_mb = epochs * (walkers * horizon // samples_per_minibatch)
+    upd_flop = epochs * walkers * horizon * FLOP_GRAD_SAMPLE + n_mb * FLOP_ADAM_MINIBATCH
+    upd_tf = upd_flop / (update_ms * 1e-3) / 1e12
+    desc = GRAD_KERNEL_DESC.get(kernel, "")
+    out = {"bound": "mfma", "kernel": f"{kernel} ({desc + ', ' if desc else ''}v_mfma_f32_16x16x4_f32)",
+           "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+           "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
+           "samples_per_launch": samples_per_minibatch, "flop_per_sample": FLOP_GRAD_SAMPLE,
+           "mean_launch_us": grad_us,
+           "mean_launch_us_per_launch_events": ev_mean_us,
+           "event_overhead_us": overhead_us,
+           "burst_us": burst_ms * 1e3, "burst_launches": GRAD_BURST,
+           "update": {"minibatches": n_mb, "flop": upd_flop, "ms": update_ms,
+                      "achieved": upd_tf, "frac": upd_tf / PEAK_FP32_TFLOPS},
+           "note": ("achieved = 36,569 flop/sample (SURVEY 8(d)) x samples per launch / the "
+                    "gradient kernel's mean in-update duration: per-launch HIP events (engine "
+                    "stream) over one real update's launches minus the per-launch event "
+                    f"overhead ({overhead_us:.2f} us: {GRAD_BURST} back-to-back launches timed "
+                    "per launch vs by one pair); burst_us is the warm back-to-back mean")}
+    per = lambda k: prof_k[k + "_ms"] / max(1, prof_k.get(k + "_launches", prof_k.get(k + "_calls", 0))) * 1e3
+    if exchange == "ipc":  # one fused launch per minibatch (profiled as the all-reduce)
+        out["reduce_exchange_adam_us"] = prof_k["allreduce_ms"] / max(1, prof_k["allreduce_calls"]) * 1e3
+    elif exchange in ("none",):
+        out["reduce_adam_us"] = per("reduce")
+    else:
+        out["reduce_us"] = per("reduce")
+        out["allreduce_us"] = prof_k["allreduce_ms"] / max(1, prof_k["allreduce_calls"]) * 1e3
+        out["adam_us"] = per("adam")
+    return out
+
+
+def flops_per_env_step(ev, policy=True):
+    """SURVEY 8(d)'s per-primitive constants priced on the counted events"""
+    f = FLOP_INTEGRATE * ev["substeps"] + FLOP_JOINT * ev["joint"] + FLOP_IMPULSE * (
+        ev["imp_ll"] + ev["imp_lf"] + ev["imp_bf"])
+    for c in ("ll", "lf", "bf"):
+        f += FLOP_SAT[c] * ev["aabb_" + c] + FLOP_CONTACT[c] * ev["sat_" + c]
+    return f / ev["env_steps"] + (FLOP_POLICY if policy else 0)
+
+
+def valu_ceiling_of(mapping):
+    """the non-FMA VALU ceiling of a rollout launch from its real grid (wk_rollout_mapping):
+    >= 2 waves per SIMD -> 78.6 T; else one wave per SIMD on the share of SIMDs holding one"""
+    waves = mapping["waves"]
     if waves >= 2 * N_SIMDS:
         return PEAK_NOFMA, "scalar non-FMA fp32 issue, >= 2 waves per SIMD"
     return (PEAK_NOFMA_ONE_WAVE * min(1.0, waves / N_SIMDS),
@@ -214,47 +276,39 @@ def valu_ceiling(lanes_per_walker, walkers):
             "(a wave64 VALU instruction per 4 cycles)")
 
 
-GRAD_KERNEL_DESC = {"k_ppo_grad_ws": "producer/consumer waves",
-                    "k_ppo_grad_tp": "tile-parallel teams of four waves, two per block",
-                    "k_ppo_grad_tp1": "tile-parallel teams of four waves, one per block"}
+KERNEL_OF_LANES = {2: "k_env_side<...,1> (pair mapping)", 4: "k_env_side<...,2> (quad mapping)",
+                   16: "k_env_step<...,16> (16-lane rows)", 1: "k_env_step<...,1> (one lane per walker)"}
 
 
-def update_roofline(prof_k, samples_per_minibatch, walkers, horizon, epochs, update_ms, burst_ms,
-                    kernel):
-    """SURVEY 8(d) update roofline: the gradient kernel (the one the update launches at this
-    minibatch, wk_grad_kernel; one launch per minibatch) priced at 36,569 flop per sample over its mean duration -- HIP events around a
-    burst of back-to-back launches (wk_time_gradient): an event pair around every launch of the
-    update adds ~4 us of event overhead to a ~35 us kernel -- and the whole update (gradient +
-    reduction + Adam over all minibatches) over its measured time"""
-    launches = max(1, prof_k.get("grad_launches", 0))
-    grad_us = burst_ms * 1e3
-    achieved = FLOP_GRAD_SAMPLE * samples_per_minibatch / (grad_us * 1e-6) / 1e12
-    n_mb = epochs * (walkers * horizon // samples_per_minibatch)
-    upd_flop = epochs * walkers * horizon * FLOP_GRAD_SAMPLE + n_mb * FLOP_ADAM_MINIBATCH
-    upd_tf = upd_flop / (update_ms * 1e-3) / 1e12
-    desc = GRAD_KERNEL_DESC.get(kernel, "")
-    return {"bound": "mfma", "kernel": f"{kernel} ({desc + ', ' if desc else ''}v_mfma_f32_16x16x4_f32)",
-            "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-            "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
-            "samples_per_launch": samples_per_minibatch, "flop_per_sample": FLOP_GRAD_SAMPLE,
-            "mean_launch_us": grad_us, "burst_launches": GRAD_BURST,
-            "mean_launch_us_per_launch_events": prof_k["grad_ms"] / launches * 1e3,
-            "reduce_adam_us": prof_k["reduce_ms"] / max(1, prof_k.get("reduce_launches", 0)) * 1e3,
-            "update": {"minibatches": n_mb, "flop": upd_flop, "ms": update_ms,
-                       "achieved": upd_tf, "frac": upd_tf / PEAK_FP32_TFLOPS},
-            "note": ("achieved = 36,569 flop/sample (SURVEY 8(d)) x samples per launch / mean "
-                     "gradient-kernel duration (one HIP-event pair on the engine stream around "
-                     f"{GRAD_BURST} back-to-back launches on minibatch 0 of the timed iteration's "
-                     "trajectory, after the timed region)")}
-
-
-def flops_per_env_step(ev):
-    """SURVEY 8(d)'s per-primitive constants priced on the counted events"""
-    f = FLOP_INTEGRATE * ev["substeps"] + FLOP_JOINT * ev["joint"] + FLOP_IMPULSE * (
-        ev["imp_ll"] + ev["imp_lf"] + ev["imp_bf"])
-    for c in ("ll", "lf", "bf"):
-        f += FLOP_SAT[c] * ev["aabb_" + c] + FLOP_CONTACT[c] * ev["sat_" + c]
-    return f / ev["env_steps"] + FLOP_POLICY
+def rollout_roofline(eng, wk, launch_ms, units, horizon, policy=True, traffic=None):
+    """the rollout kernel's roofline on THIS context: its physics events counted by replaying the
+    timed iteration's actions (restore -> wk_count_events) and priced with SURVEY 8(d)'s
+    constants, over the mean launch time (HIP events on the engine stream, profile level 1)"""
+    eng.restore()
+    ev = dict(zip(wk.EVENTS, eng.count_events(horizon).tolist()))
+    f = flops_per_env_step(ev, policy)
+    achieved = f * units / (launch_ms * 1e-3) / 1e12
+    mp = eng.rollout_mapping()
+    ceiling, why = valu_ceiling_of(mp)
+    return {
+        "bound": "valu",
+        "kernel": (KERNEL_OF_LANES[mp["lanes_per_walker"]]
+                   + (" fused rollout: physics + matrix-core policy" if policy else " physics only")),
+        "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+        "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
+        "peak_no_fma": ceiling, "frac_no_fma": achieved / ceiling, "peak_no_fma_basis": why,
+        "mapping": mp,
+        "flop_per_env_step_counted": f, "flop_per_env_step_upper_bound": FLOP_UPPER,
+        "events_per_env_step": {k: v / ev["env_steps"] for k, v in ev.items() if k != "env_steps"},
+        "env_steps_per_launch": units, "mean_launch_ms": launch_ms,
+        "hbm_GBs": (traffic / (launch_ms * 1e-3) / 1e9) if traffic else None,
+        "hbm_frac": (traffic / (launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBS) if traffic else None,
+        "alg_bytes_per_launch": (alg_bytes_per_env_step(horizon) if policy else 0.0) * units,
+        "note": (f"VALU-issue bound (op-for-op fp32 restatement, no FMA contraction); achieved = "
+                 f"F_counted {f:.0f} flop/env-step (SURVEY 8(d) constants priced on this "
+                 f"iteration's counted AABB/SAT/contact/impulse/joint events) x {units:.0f} "
+                 f"env-steps per launch / {launch_ms:.3f} ms mean launch (HIP events on the "
+                 "engine stream)")}
 
 
 def time_iterations(eng, args, k, horizon, update_index, barrier=None, physics_only=None):
@@ -281,13 +335,15 @@ def time_iterations(eng, args, k, horizon, update_index, barrier=None, physics_o
 
 def extra_config(wk, torch, args, n, M, M_global, horizon, physics_only=False, materials=False,
                  k=5, rough=False):
-    """one of BASELINE's other shapes on this GPU (same regime protocol as the main line);
-    rough: the same loop on CreateRoughFloor's terrain"""
+    """one of BASELINE's other shapes on this GPU (same regime protocol as the main line), with
+    its own rollout roofline and update roofline; rough: the same loop on
+    CreateRoughFloor's terrain"""
     eng = wk.Engine(n, seed=args.seed, Horizon=horizon, Minibatch=M, MinibatchGlobal=M_global,
                     Epochs=args.epochs, RandomizeStart=1, RandomizeMaterial=int(materials),
                     LanesPerWalker=args.lanes, RoughFloor=int(rough))
     try:
         if physics_only:
+            import numpy as np
             g = torch.Generator(device="cuda").manual_seed(args.seed)
             acts = torch.rand((horizon, n, 4), device="cuda", generator=g) * 2 - 1
             rew = torch.empty((horizon, n), device="cuda")
@@ -297,9 +353,23 @@ def extra_config(wk, torch, args, n, M, M_global, horizon, physics_only=False, m
                                            done.data_ptr(), None)
             eng.snapshot()
             time_iterations(eng, args, 2, horizon, 0, physics_only=step)  # warm-up
-            dt = time_iterations(eng, args, 16, horizon, 0, physics_only=step)
-            return {"walkers": n, "env_steps_timed": 16 * n * horizon,
-                    "env_steps_per_s": 16 * n * horizon / dt}
+            reps = 16
+            eng.profile_reset()
+            eng.profile_enable(1)
+            dt = time_iterations(eng, args, reps, horizon, 0, physics_only=step)
+            prof = eng.profile()
+            eng.profile_enable(0)
+            launch_ms = prof["physics_ms"] / max(1, prof["physics_launches"])
+            # the counting replay reads the trajectory buffer's actions: the same uniform
+            # actions every timed launch stepped with, from the same restored state
+            z = lambda *sh: np.zeros(sh, np.float32)
+            eng.set_trajectory(z(horizon, n, 12), acts.cpu().numpy(), z(horizon, n, 4),
+                               z(horizon, n), np.zeros((horizon, n), np.uint8), z(horizon, n))
+            return {"walkers": n, "env_steps_timed": reps * n * horizon,
+                    "env_steps_per_s": reps * n * horizon / dt,
+                    "physics_ms_per_launch": launch_ms,
+                    "roofline": rollout_roofline(eng, wk, launch_ms, n * horizon, horizon,
+                                                 policy=False)}
         for it in range(args.regime_iters):
             eng.rollout(horizon)
             eng.ppo_update(update_index=it, sync=False)
@@ -317,15 +387,17 @@ def extra_config(wk, torch, args, n, M, M_global, horizon, physics_only=False, m
         prof_k = eng.profile()
         upd_ms = prof["update_ms"] / max(1, prof["update_calls"])
         burst = eng.time_gradient(M, GRAD_BURST)
+        burst_ev = eng.time_gradient(M, GRAD_BURST, per_launch_events=True)
+        launch_ms = prof["physics_ms"] / max(1, prof["physics_launches"])
         return {"walkers": n, "minibatch": M, "minibatch_global": M_global,
                 "env_steps_per_s": k * n * horizon / dt,
-                "rollout_ms": prof["physics_ms"] / max(1, prof["physics_launches"]),
-                "rollout_env_steps_per_s": n * horizon * prof["physics_launches"]
-                / max(1e-9, prof["physics_ms"] * 1e-3),
+                "rollout_ms": launch_ms,
+                "rollout_env_steps_per_s": n * horizon / max(1e-12, launch_ms * 1e-3),
                 "ppo_update_ms": upd_ms,
                 "minibatches_per_update": args.epochs * (n * horizon // M),
+                "roofline": rollout_roofline(eng, wk, launch_ms, n * horizon, horizon),
                 "roofline_update": update_roofline(prof_k, M, n, horizon, args.epochs, upd_ms, burst,
-                                                   eng.grad_kernel(M))}
+                                                   burst_ev, eng.grad_kernel(M))}
     finally:
         eng.close()
 
@@ -358,6 +430,83 @@ def allreduce_one_rank(wk, eng, args, horizon, update_index):
             "ms_per_update": p["allreduce_ms"] / 2, "update_ms": p["update_ms"] / 2,
             "kernel_ms_one_step": {k: v / 2 for k, v in p.items() if k.endswith("_ms")},
             "note": "one-rank RCCL communicator on this GPU: the collective path of every rank"}
+
+
+def ipc_exchange_setup(wk, eng, mk_engine, rank, world, horizon, dist, torch, np):
+    """N > 1 with --exchange ipc: map the peers' exchange regions (every rank joins
+    the record all-gather, also when its own handle failed), run one test round on exact small
+    integers, vote; then check the one-shot exchange against an EXACT reference over several
+    updates: a second context on the same shard whose host exchange all-gathers the slabs over
+    gloo and sums them in rank order in float32 (the IPC kernel's association, so the result is
+    bit-identical whatever N) -- two PPO iterations of 2 epochs each from the seeded start, then
+    the weights, Adam moments and walker records compared bit for bit, and the replicas'
+    weights compared across ranks.  Any failure returns 0 (bench.py then falls back to RCCL on
+    every rank).  The IPC context is restored to its seeded start afterwards."""
+    def allgather(b):
+        out = [None] * world
+        dist.all_gather_object(out, b)
+        return out
+
+    def vote(ok):
+        t = torch.tensor([int(ok)])
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    check = {"test_round": False, "checked": False}
+    ok = True
+    try:
+        eng.comm_init_ipc(rank, world, allgather)
+        check["region"] = "uncached device memory" if eng.comm_info()[1] else "hipMalloc"
+        base = (np.arange(wk.NPARAM) % 97).astype(np.float32)
+        got = eng.allreduce_test(base + np.float32(rank + 1))
+        want = base * np.float32(world) + np.float32(world * (world + 1) // 2)
+        ok = bool(np.array_equal(got, want))
+        if not ok:
+            print(f"rank {rank}: IPC exchange test gave wrong sums", file=sys.stderr)
+    except wk.WkError as ex:  # e.g. no peer access between the devices, a peer timed out
+        print(f"rank {rank}: IPC exchange unavailable ({ex})", file=sys.stderr)
+        ok = False
+    if not vote(ok):
+        return 0, check
+    check["test_round"] = True
+
+    def rank_order_sum(buf):
+        t = torch.from_numpy(buf.copy())
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        acc = parts[0].numpy().copy()
+        for p in parts[1:]:
+            acc = acc + p.numpy()  # float32, rank order
+        buf[:] = acc
+
+    ref = mk_engine()
+    try:
+        ref.comm_init_host(rank, world, rank_order_sum)
+        eng.snapshot()
+        updates, epochs = 2, 2
+        for u in range(updates):
+            for e in (eng, ref):
+                e.rollout(horizon)
+                e.ppo_update(epochs=epochs, update_index=1000 + u)
+        w, (m, v, t) = eng.get_weights(), eng.get_adam()
+        same = (np.array_equal(w, ref.get_weights()) and np.array_equal(m, ref.get_adam()[0])
+                and np.array_equal(v, ref.get_adam()[1]) and t == ref.get_adam()[2]
+                and np.array_equal(eng.get_state(), ref.get_state()))
+        replicas = allgather(w.tobytes())
+        identical = all(r == replicas[0] for r in replicas)
+        eng.restore()
+    except wk.WkError as ex:
+        print(f"rank {rank}: IPC exchange check failed ({ex})", file=sys.stderr)
+        same, identical, t = False, False, 0
+    finally:
+        ref.close()
+    check.update({"checked": True, "updates": updates, "epochs_per_update": epochs,
+                  "adam_steps": int(t), "bitwise_equal_to_reference": bool(same),
+                  "replicas_identical": bool(identical),
+                  "reference": "rank-order float32 sum of the ranks' slabs all-gathered over gloo"})
+    if not (same and identical):
+        print(f"rank {rank}: IPC exchange differs from the rank-order reference", file=sys.stderr)
+    return int(same and identical), check
 
 
 def main():
@@ -397,48 +546,32 @@ def main():
         raise SystemExit("the global minibatch must divide by the number of GPUs")
     shard = make_shard(rank, world, local, n_local, m_global // world)
     T = args.horizon
-    eng = wk.Engine(shard.n_local, seed=args.seed, device=local, Horizon=T,
-                    Minibatch=shard.minibatch_local, MinibatchGlobal=shard.minibatch_global,
-                    Epochs=args.epochs, EnvOffset=shard.env_offset, RandomizeStart=1,
-                    RandomizeMaterial=1 if args.materials else 0, LanesPerWalker=args.lanes)
+    mk_engine = lambda: wk.Engine(
+        shard.n_local, seed=args.seed, device=local, Horizon=T, Minibatch=shard.minibatch_local,
+        MinibatchGlobal=shard.minibatch_global, Epochs=args.epochs, EnvOffset=shard.env_offset,
+        RandomizeStart=1, RandomizeMaterial=1 if args.materials else 0, LanesPerWalker=args.lanes)
+    eng = mk_engine()
     exchange = args.exchange if world > 1 else "none"
+    xch_check = None
     if world > 1 and args.exchange == "ipc":
-        def allgather(b):
-            out = [None] * world
-            dist.all_gather_object(out, b)
-            return out
-        try:
-            eng.comm_init_ipc(rank, world, allgather)
-            # one test round on exact small integers: every rank must see the sum of all
-            # ranks' values (a mapping that cannot be read, or a peer that never publishes,
-            # falls back to RCCL here rather than stalling the timed run)
-            base = (np.arange(wk.NPARAM) % 97).astype(np.float32)
-            got = eng.allreduce_test(base + np.float32(rank + 1))
-            want = base * np.float32(world) + np.float32(world * (world + 1) // 2)
-            ok = 1 if np.array_equal(got, want) else 0
-            if not ok:
-                print(f"rank {rank}: IPC exchange test gave wrong sums; using RCCL", file=sys.stderr)
-        except wk.WkError as ex:  # e.g. no peer access between the devices
-            print(f"rank {rank}: IPC exchange unavailable ({ex}); using RCCL", file=sys.stderr)
-            ok = 0
+        ok, xch_check = ipc_exchange_setup(wk, eng, mk_engine, rank, world, T, dist, torch, np)
         okt = torch.tensor([ok])
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)  # every rank takes the same exchange
         if not okt.item():
             eng.close()
-            eng = wk.Engine(shard.n_local, seed=args.seed, device=local, Horizon=T,
-                            Minibatch=shard.minibatch_local, MinibatchGlobal=shard.minibatch_global,
-                            Epochs=args.epochs, EnvOffset=shard.env_offset, RandomizeStart=1,
-                            RandomizeMaterial=1 if args.materials else 0, LanesPerWalker=args.lanes)
+            eng = mk_engine()
             exchange = "host (gloo)" if args.rehearse else "rccl"
     if world > 1 and exchange != "ipc" and args.rehearse:
         def host_allreduce(buf):
             t = torch.from_numpy(buf)
             dist.all_reduce(t)  # in place on the numpy view (gloo)
         eng.comm_init_host(rank, world, host_allreduce)
+        exchange = "host (gloo)"
     elif world > 1 and exchange != "ipc":
         uid = wk.Engine.comm_unique_id() if rank == 0 else None
         uid = broadcast_unique_id(uid)
         eng.comm_init(rank, world, uid)
+        exchange = "rccl"
 
     def barrier():
         torch.cuda.synchronize()
@@ -464,14 +597,16 @@ def main():
     time_iterations(eng, args, 1, T, upd)
     eng.profile_enable(0)
     prof_k = eng.profile()
-    # untimed: the gradient kernel alone, back to back (the update roofline's duration)
+    # untimed: the gradient kernel alone, back to back, timed by one event pair and by a pair
+    # around every launch (their difference: the per-launch event overhead, subtracted from the
+    # level-2 in-update mean for the update roofline)
     grad_burst_ms = eng.time_gradient(shard.minibatch_local, GRAD_BURST)
-    # untimed: the same rollout's physics events (counting replay of its actions)
+    grad_burst_ev_ms = eng.time_gradient(shard.minibatch_local, GRAD_BURST, per_launch_events=True)
+    # untimed: the timed iteration's episode count, then its physics events (counting replay of
+    # its actions from the restored state) for the rollout roofline
     eng.restore()
     eng.rollout(T)
     stats = eng.rollout_stats()
-    eng.restore()
-    ev = dict(zip(wk.EVENTS, eng.count_events(T).tolist()))
 
     t = torch.tensor([elapsed, prof["physics_ms"], prof["update_ms"]], dtype=torch.float64)
     if world > 1:
@@ -482,8 +617,6 @@ def main():
     value = env_steps / elapsed
     launch_ms = prof["physics_ms"] / max(1, prof["physics_launches"])
     units = prof["physics_env_steps"] / max(1, prof["physics_launches"])
-    f_counted = flops_per_env_step(ev)
-    achieved = f_counted * units / (launch_ms * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_file):
         try:
@@ -492,13 +625,7 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
-    # the mapping wk_create picks (include/wk_api.h, LanesPerWalker 0 = auto)
-    lanes = args.lanes or (4 if shard.n_local <= 16384 else 2)
-    ceiling, ceiling_why = valu_ceiling(lanes, shard.n_local)
-    kernel = {2: "k_env_side<true,true,false,1>", 4: "k_env_side<true,true,false,2> (quad mapping)",
-              16: "k_env_step<true,true,false,16,false>",
-              1: "k_env_step<true,true,false,1,false>"}[lanes]
-    alg_bytes = alg_bytes_per_env_step(T) * units
+    roofline = rollout_roofline(eng, wk, launch_ms, units, T, traffic=traffic)
     out = {
         "metric": METRIC,
         "value": value,
@@ -524,42 +651,21 @@ def main():
             "epochs": args.epochs,
             "minibatch_global": shard.minibatch_global,
             "parallelism": f"dp{world}",
-            "exchange": (exchange if exchange in ("none", "ipc")
-                         else "host (gloo)" if args.rehearse else "rccl"),
+            "exchange": exchange,
         },
         "ppo_update_ms": upd_ms_max / args.steps,
         "rollout_env_steps_per_s": world * shard.n_local * T * args.steps / (phys_ms_max * 1e-3),
         "regime": {"iterations_before_snapshot": args.regime_iters,
                    "episodes_per_rollout": int(stats.episodes)},
-        "roofline": {
-            "bound": "valu",
-            "kernel": kernel + " (fused rollout: physics + matrix-core policy)",
-            "achieved": achieved,
-            "peak": PEAK_FP32_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": achieved / PEAK_FP32_TFLOPS,
-            "traffic": traffic,
-            "peak_no_fma": ceiling,
-            "frac_no_fma": achieved / ceiling,
-            "peak_no_fma_basis": ceiling_why,
-            "flop_per_env_step_counted": f_counted,
-            "flop_per_env_step_upper_bound": FLOP_UPPER,
-            "events_per_env_step": {k: v / ev["env_steps"] for k, v in ev.items()
-                                    if k != "env_steps"},
-            "hbm_GBs": (traffic / (launch_ms * 1e-3) / 1e9) if traffic else None,
-            "hbm_frac": (traffic / (launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBS) if traffic else None,
-            "alg_bytes_per_launch": alg_bytes,
-            "note": ("VALU-issue bound (op-for-op fp32 restatement, no FMA contraction); achieved = "
-                     f"F_counted {f_counted:.0f} flop/env-step (SURVEY 8(d) constants priced on "
-                     f"this rollout's counted AABB/SAT/contact/impulse/joint events) x "
-                     f"{units:.0f} env-steps per launch / {launch_ms:.3f} ms mean launch (HIP "
-                     "events on the engine stream)"),
-        },
+        "roofline": roofline,
         "kernel_ms_one_step": {k: v for k, v in prof_k.items() if k.endswith("_ms")},
         "roofline_update": update_roofline(prof_k, shard.minibatch_local, shard.n_local, T,
                                            args.epochs, upd_ms_max / args.steps, grad_burst_ms,
-                                           eng.grad_kernel(shard.minibatch_local)),
+                                           grad_burst_ev_ms, eng.grad_kernel(shard.minibatch_local),
+                                           exchange),
     }
+    if xch_check is not None:
+        out["config"]["exchange_check"] = xch_check
     if world == 1 and not args.rehearse:
         out["allreduce_1rank"] = allreduce_one_rank(wk, eng, args, T, upd)
     if rank == 0 and world == 1 and not args.no_extras:
@@ -577,7 +683,7 @@ def main():
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if args.rehearse:
-        out["rehearsal"] = ("all ranks on one GPU, host all-reduce over gloo: a check of the "
+        out["rehearsal"] = (f"all ranks on one GPU, exchange {exchange}: a check of the "
                             "multi-rank path, not a performance number")
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)

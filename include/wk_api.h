@@ -385,15 +385,25 @@ int wk_allreduce_test(wk_ctx* ctx, float* host_buf, int n);
 typedef int (*wk_host_allreduce_fn)(float* buf, int n, void* user);
 int wk_comm_init_host(wk_ctx* ctx, int rank, int nranks, wk_host_allreduce_fn fn, void* user);
 /* The one-shot exchange over peer-mapped memory instead of RCCL (ranks on one node, at most 8):
- * wk_comm_ipc_handle allocates this rank's exchange region and returns its IPC handle; the
- * caller all-gathers the handles (any control plane) and passes all of them, in rank order, to
- * wk_comm_init_ipc, which maps the peers' regions.  Per minibatch one kernel publishes this
- * rank's ordered block sum, waits (bounded, ~1 s) for every peer's, sums the ranks' slabs in
- * rank order and applies Adam -- no collective library, no host round trip.  A peer that never
- * publishes fails wk_ppo_update with WK_ERR_COMM (fatal for the job, as a failed all-reduce). */
-enum { WK_IPC_HANDLE_BYTES = 64 };
+ * wk_comm_ipc_handle allocates this rank's exchange region and returns its record (the IPC
+ * handle, then the PCI bus id of the rank's GPU); the caller all-gathers the records (any
+ * control plane) and passes all of them, in rank order, to wk_comm_init_ipc, which maps the
+ * peers' regions (WK_ERR_ARG if more than 4 ranks share one GPU: they would stall).  Per
+ * minibatch one kernel publishes this rank's ordered block sum, waits (bounded: 2 s of the
+ * GPU's constant clock) for every peer's, sums the ranks' slabs in rank order and applies
+ * Adam -- no collective library, no host round trip.  A peer that never publishes fails
+ * wk_ppo_update / wk_train_batch / wk_minibatch_gradient / wk_allreduce_test with WK_ERR_COMM
+ * (fatal for the job, as a failed all-reduce): from the timed-out minibatch on no Adam step is
+ * applied (W, m, v keep the last good minibatch's values) and no later exchange publishes, so
+ * the peers time out too.  wk_minibatch_gradient and wk_train_batch(apply_adam = 0) run the
+ * exchange as well (collective calls: every rank must make them), returning the sum over the
+ * ranks as on an RCCL context. */
+enum { WK_IPC_HANDLE_BYTES = 128 };
 int wk_comm_ipc_handle(wk_ctx* ctx, uint8_t* handle /* WK_IPC_HANDLE_BYTES */);
-int wk_comm_init_ipc(wk_ctx* ctx, int rank, int nranks, const uint8_t* handles /* nranks * 64 */);
+int wk_comm_init_ipc(wk_ctx* ctx, int rank, int nranks, const uint8_t* handles /* nranks * 128 */);
+/* the context's minibatch exchange: *kind 0 none, 1 RCCL, 2 host callback, 3 IPC; *flags bit 0:
+ * the IPC exchange region is uncached device memory (else coarse-grained hipMalloc memory) */
+int wk_comm_info(wk_ctx* ctx, int* kind, int* flags);
 
 /* profiling */
 /* level 0 off; 1: HIP events around each rollout / returns pass / whole PPO update (cheap
@@ -428,6 +438,16 @@ int wk_snapshot(wk_ctx* ctx, int op);
  * timed by one HIP-event pair on the context's stream -- the kernel's mean duration without
  * per-launch event overhead (bench.py's update roofline).  Writes only scratch slabs. */
 int wk_time_gradient(wk_ctx* ctx, int minibatch, int reps, double* ms_per_launch);
+/* The same with flags: bit 0 puts an event pair around EVERY launch (the elapsed times summed),
+ * as profile level 2 times each launch of the update.  bench.py prices the update roofline on
+ * the gradient kernel's in-update duration: the level-2 per-launch mean inside a real update
+ * minus the per-launch event overhead (this burst with bit 0 minus the plain burst). */
+int wk_time_gradient_ex(wk_ctx* ctx, int minibatch, int reps, int flags, double* ms_per_launch);
+
+/* The rollout kernel's mapping as launched: lanes per walker (1, 2, 4 or 16), walkers per
+ * wave (fewer than 64 / lanes for the sparse quad mapping) and the wave count of one rollout
+ * launch -- bench.py's VALU ceiling (one wave per SIMD below 1,024 waves). */
+int wk_rollout_mapping(wk_ctx* ctx, int* lanes_per_walker, int* walkers_per_wave, int64_t* waves);
 
 /* Which matrix-core gradient kernel the update launches for a per-GPU minibatch of `minibatch`
  * samples (0 = config Minibatch): 0 producer / consumer waves (k_ppo_grad_ws), 1 tile-parallel

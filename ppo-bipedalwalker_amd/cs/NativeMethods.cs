@@ -23,6 +23,7 @@ public static class WkConst
 {
     public const int StateFloats = 112, NParam = 6149, NParamCritic = 897, NParamActor = 5252;
     public const int Obs = 12, Act = 4, NPairs = 9, MaxProps = 4, PropMaxV = 24, NEvents = 16;
+    public const int IpcHandleBytes = 128;  // WK_IPC_HANDLE_BYTES: IPC handle + the GPU's PCI bus id
 }
 
 // Hyperparameters.cs:80-121 names and defaults (wk_config_defaults) + the batched extensions
@@ -206,6 +207,7 @@ public static class Wk
     [DllImport(Lib)] public static extern int wk_allreduce_test(IntPtr ctx, float[] buf, int n);
     [DllImport(Lib)] public static extern int wk_comm_ipc_handle(IntPtr ctx, byte[] handle);
     [DllImport(Lib)] public static extern int wk_comm_init_ipc(IntPtr ctx, int rank, int nRanks, byte[] handles);
+    [DllImport(Lib)] public static extern int wk_comm_info(IntPtr ctx, out int kind, out int flags);
     [UnmanagedFunctionPointer(CallingConvention.Cdecl)] public delegate int HostAllReduce(IntPtr buf, int n, IntPtr user);
     [DllImport(Lib)] public static extern int wk_comm_init_host(IntPtr ctx, int rank, int nRanks, HostAllReduce fn, IntPtr user);
 
@@ -235,6 +237,8 @@ public static class Wk
     [DllImport(Lib)] public static extern int wk_count_events(IntPtr ctx, int k, ulong[] counts);
     [DllImport(Lib)] public static extern int wk_snapshot(IntPtr ctx, int op);
     [DllImport(Lib)] public static extern int wk_time_gradient(IntPtr ctx, int minibatch, int reps, out double msPerLaunch);
+    [DllImport(Lib)] public static extern int wk_time_gradient_ex(IntPtr ctx, int minibatch, int reps, int flags, out double msPerLaunch);
+    [DllImport(Lib)] public static extern int wk_rollout_mapping(IntPtr ctx, out int lanesPerWalker, out int walkersPerWave, out long waves);
     [DllImport(Lib)] public static extern int wk_grad_kernel(IntPtr ctx, int minibatch);
 
     public static string LastError(IntPtr ctx) => Marshal.PtrToStringAnsi(wk_last_error(ctx)) ?? "";

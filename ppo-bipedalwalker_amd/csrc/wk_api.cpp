@@ -96,6 +96,7 @@ struct wk_ctx {
   bool ipc = false;
   uint64_t xch_seq = 0;
   uint32_t* xch_err = nullptr;         // device word: a peer never published
+  bool xch_uncached = false;           // the region is uncached device memory (else hipMalloc)
   // profiling
   int prof = 0;  // profile level
   struct Ev { int kind; hipEvent_t a, b; int64_t units; };
@@ -1028,7 +1029,10 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   // with a communicator (any size, also one rank) the collective path runs: reduction,
   // RCCL all-reduce, Adam -- a single-GPU test then covers the multi-GPU sequence
   const bool multi = c->comm != nullptr || c->host_ar != nullptr || c->ipc;
-  if (c->ipc && apply_adam) {  // reduction, exchange and Adam in one launch (k_reduce_xch_adam)
+  // reduction, exchange and Adam in one launch (k_reduce_xch_adam); a gradient-only call
+  // (apply_adam 0: a.W == null) runs the exchange alone, so on every kind of context the
+  // returned gradient is the sum over the ranks
+  if (c->ipc) {
     ProfScope ps(c, PK_ALLRED, 0, 2);
     wk::XchArgs x = c->xa;
     x.partial = c->partial;
@@ -1050,7 +1054,7 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
     HIPCHK(c, wk::launch_grad_reduce(c->partial, nblocks, part2, c->grad, c->stream));
   }
 
-  if (multi && !c->ipc) {  // (a gradient-only call on an IPC context keeps the local sum)
+  if (multi) {
     ProfScope ps(c, PK_ALLRED, 0, 2);
     if (c->comm) {
       ncclResult_t r = ncclAllReduce(c->grad, c->grad, wk::SLAB, ncclFloat, ncclSum,
@@ -1077,6 +1081,21 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   return WK_OK;
 }
 
+// IPC contexts: WK_ERR_COMM once an exchange timed out (a peer never published; from then on
+// every exchange is a no-op and the weights keep the last good minibatch's values)
+static int xch_status(wk_ctx* c) {
+  if (!c->ipc) return WK_OK;
+  uint32_t err = 0;
+  HIPCHK(c, hipMemcpyAsync(&err, c->xch_err, sizeof err, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (err) {
+    SETERR(c, "IPC gradient exchange: a peer did not publish its minibatch slab within %.0f s "
+           "(no Adam step applied since)", (double)wk::XCH_TIMEOUT_TICKS / 1e8);
+    return WK_ERR_COMM;
+  }
+  return WK_OK;
+}
+
 static wk::GradArgs grad_base(wk_ctx* c) {
   wk::GradArgs g{};
   g.W = c->W;
@@ -1098,9 +1117,32 @@ int wk_grad_kernel(wk_ctx* c, int minibatch) {
   return wk::grad_impl_for(c->grad_impl, minibatch > 0 ? minibatch : c->cfg.Minibatch);
 }
 
+int wk_rollout_mapping(wk_ctx* c, int* lanes_per_walker, int* walkers_per_wave, int64_t* waves) {
+  if (!c || !lanes_per_walker || !walkers_per_wave || !waves) return WK_ERR_ARG;
+  const int64_t n = c->n;
+  if (c->scene.n_props > 0) {  // the one-lane scene kernel
+    *lanes_per_walker = 1; *walkers_per_wave = 64; *waves = (n + 63) / 64;
+    return WK_OK;
+  }
+  const int L = c->P.lanes;
+  *lanes_per_walker = L;
+  if (L == 4) {  // sparse quad: wpw walkers in the first 4 wpw lanes of each wave
+    *walkers_per_wave = c->P.wpw;
+    *waves = (n + c->P.wpw - 1) / c->P.wpw;
+  } else {
+    *walkers_per_wave = 64 / L;
+    *waves = (n * L + 63) / 64;
+  }
+  return WK_OK;
+}
+
 int wk_time_gradient(wk_ctx* c, int minibatch, int reps, double* ms_per_launch) {
+  return wk_time_gradient_ex(c, minibatch, reps, 0, ms_per_launch);
+}
+
+int wk_time_gradient_ex(wk_ctx* c, int minibatch, int reps, int flags, double* ms_per_launch) {
   DevGuard dg_(c);
-  if (!c || reps <= 0 || !ms_per_launch) return WK_ERR_ARG;
+  if (!c || reps <= 0 || !ms_per_launch || (flags & ~1)) return WK_ERR_ARG;
   if (c->T_valid <= 0) { SETERR(c, "wk_time_gradient before wk_rollout / wk_set_trajectory"); return WK_ERR_STATE; }
   if (!c->returns_valid) {
     int r = returns_impl(c);
@@ -1128,19 +1170,27 @@ int wk_time_gradient(wk_ctx* c, int minibatch, int reps, double* ms_per_launch) 
     c->partial_floats = need;
   }
   g.partial = c->partial;
-  hipEvent_t a = nullptr, b = nullptr;
-  HIPCHK(c, hipEventCreate(&a));
-  HIPCHK(c, hipEventCreate(&b));
   HIPCHK(c, wk::launch_ppo_grad_mfma(g, nblocks, gi, c->stream));  // warm
-  HIPCHK(c, hipEventRecord(a, c->stream));
-  for (int i = 0; i < reps; i++) HIPCHK(c, wk::launch_ppo_grad_mfma(g, nblocks, gi, c->stream));
-  HIPCHK(c, hipEventRecord(b, c->stream));
-  HIPCHK(c, hipEventSynchronize(b));
-  float ms = 0.0f;
-  HIPCHK(c, hipEventElapsedTime(&ms, a, b));
-  (void)hipEventDestroy(a);
-  (void)hipEventDestroy(b);
-  *ms_per_launch = (double)ms / reps;
+  // flags & 1: an event pair around EVERY launch (as profile level 2 times the update's
+  // launches), the elapsed times summed -- the burst's per-launch event overhead is the
+  // difference to one pair around the whole burst
+  const int npairs = (flags & 1) ? reps : 1;
+  std::vector<hipEvent_t> ev(2 * (size_t)npairs, nullptr);
+  for (auto& e : ev) HIPCHK(c, hipEventCreate(&e));
+  for (int i = 0; i < reps; i++) {
+    if ((flags & 1) || i == 0) HIPCHK(c, hipEventRecord(ev[2 * ((flags & 1) ? i : 0)], c->stream));
+    HIPCHK(c, wk::launch_ppo_grad_mfma(g, nblocks, gi, c->stream));
+    if ((flags & 1) || i == reps - 1) HIPCHK(c, hipEventRecord(ev[2 * ((flags & 1) ? i : 0) + 1], c->stream));
+  }
+  HIPCHK(c, hipEventSynchronize(ev.back()));
+  double total = 0.0;
+  for (int i = 0; i < npairs; i++) {
+    float ms = 0.0f;
+    HIPCHK(c, hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+    total += ms;
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  *ms_per_launch = total / reps;
   return WK_OK;
 }
 
@@ -1153,11 +1203,9 @@ int wk_ppo_update(wk_ctx* c, const wk_ppo_args* args, float* critic_diag, float*
     int r = ppo_update_impl(c, args);
     if (r) return r;
   }
-  if (c->ipc) {  // a peer that never published is fatal for the job (like a failed all-reduce)
-    uint32_t err = 0;
-    HIPCHK(c, hipMemcpyAsync(&err, c->xch_err, sizeof err, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (err) { SETERR(c, "IPC gradient exchange: a peer did not publish its minibatch slab"); return WK_ERR_COMM; }
+  {  // a peer that never published is fatal for the job (like a failed all-reduce)
+    int r = xch_status(c);
+    if (r) return r;
   }
   if (c->collect) {  // the last minibatch's losses, as PPOAgent.Train hands them on (:165-166)
     if (c->loss_count < c->loss_cap)
@@ -1238,6 +1286,8 @@ static int batch_impl(wk_ctx* c, int wpb, int B, float b_div, const float* s, co
   std::vector<float> slab(wk::SLAB);
   HIPCHK(c, hipMemcpyAsync(slab.data(), c->grad, sizeof(float) * slab.size(), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  r = xch_status(c);  // (IPC: a timed-out exchange left grad stale and applied no Adam)
+  if (r) return r;
   if (grads_out) memcpy(grads_out, slab.data(), sizeof(float) * wk::NPARAM);
   if (cd) *cd = slab[wk::NPARAM];
   if (ad) *ad = slab[wk::NPARAM + 1];
@@ -1294,19 +1344,40 @@ int wk_comm_init_host(wk_ctx* c, int rank, int nranks, wk_host_allreduce_fn fn, 
   return WK_OK;
 }
 
+// the exchange record of one rank: [0, 64) the region's hipIpcMemHandle_t, [64, 128) the PCI bus
+// id of the rank's device (NUL-padded), so every rank can count the ranks sharing its GPU
+static constexpr size_t kIpcDevOff = 64;
+static_assert(sizeof(hipIpcMemHandle_t) == kIpcDevOff && WK_IPC_HANDLE_BYTES == 128, "IPC record");
+
 int wk_comm_ipc_handle(wk_ctx* c, uint8_t* handle) {
   DevGuard dg_(c);
   if (!c || !handle) return WK_ERR_ARG;
-  static_assert(sizeof(hipIpcMemHandle_t) == WK_IPC_HANDLE_BYTES, "IPC handle size");
   if (!c->xch) {
-    HIPCHK(c, hipMalloc(&c->xch, wk::xch_region_bytes()));
-    HIPCHK(c, hipMemset(c->xch, 0, wk::xch_region_bytes()));
+    // uncached (MTYPE UC) device memory: the peers read it over xGMI and this GPU writes it
+    // through no cache; coarse-grained hipMalloc memory is the fallback where the driver cannot
+    // export an uncached allocation (the system-scope release / acquire covers it as well)
+    const size_t bytes = wk::xch_region_bytes();
+    hipIpcMemHandle_t probe;
+    if (hipExtMallocWithFlags(&c->xch, bytes, hipDeviceMallocUncached) != hipSuccess ||
+        hipIpcGetMemHandle(&probe, c->xch) != hipSuccess) {
+      if (c->xch) (void)hipFree(c->xch);
+      c->xch = nullptr;
+      (void)hipGetLastError();
+      HIPCHK(c, hipMalloc(&c->xch, bytes));
+      c->xch_uncached = false;
+    } else {
+      c->xch_uncached = true;
+    }
+    HIPCHK(c, hipMemset(c->xch, 0, bytes));
     HIPCHK(c, hipMalloc((void**)&c->xch_err, sizeof(uint32_t)));
     HIPCHK(c, hipMemset(c->xch_err, 0, sizeof(uint32_t)));
   }
   hipIpcMemHandle_t h;
   HIPCHK(c, hipIpcGetMemHandle(&h, c->xch));
+  memset(handle, 0, WK_IPC_HANDLE_BYTES);
   memcpy(handle, &h, sizeof h);
+  HIPCHK(c, hipDeviceGetPCIBusId((char*)handle + kIpcDevOff, (int)(WK_IPC_HANDLE_BYTES - kIpcDevOff) - 1,
+                                 c->device));
   return WK_OK;
 }
 
@@ -1316,6 +1387,19 @@ int wk_comm_init_ipc(wk_ctx* c, int rank, int nranks, const uint8_t* handles) {
   if (nranks > wk::XCH_MAX_RANKS) { SETERR(c, "the IPC exchange spans at most %d ranks", (int)wk::XCH_MAX_RANKS); return WK_ERR_ARG; }
   if (c->comm || c->host_ar || c->ipc) { SETERR(c, "the context already has an all-reduce"); return WK_ERR_STATE; }
   if (!c->xch) { SETERR(c, "wk_comm_ipc_handle first"); return WK_ERR_STATE; }
+  {  // ranks sharing this rank's GPU (a rehearsal): more than four stall, see XCH_MAX_RANKS_PER_DEVICE
+    const char* mine = (const char*)handles + (size_t)rank * WK_IPC_HANDLE_BYTES + kIpcDevOff;
+    int same = 0;
+    for (int r = 0; r < nranks; r++)
+      same += strncmp(mine, (const char*)handles + (size_t)r * WK_IPC_HANDLE_BYTES + kIpcDevOff,
+                      WK_IPC_HANDLE_BYTES - kIpcDevOff) == 0;
+    if (same > wk::XCH_MAX_RANKS_PER_DEVICE) {
+      SETERR(c, "the IPC exchange takes at most %d ranks per GPU (%d share %s): their waiting "
+             "exchange blocks would hold the CUs a peer's gradient kernel needs",
+             (int)wk::XCH_MAX_RANKS_PER_DEVICE, same, mine);
+      return WK_ERR_ARG;
+    }
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   wk::XchArgs x{};
   std::vector<void*> opened;
@@ -1345,6 +1429,13 @@ int wk_comm_init_ipc(wk_ctx* c, int rank, int nranks, const uint8_t* handles) {
   return WK_OK;
 }
 
+int wk_comm_info(wk_ctx* c, int* kind, int* flags) {
+  if (!c || !kind || !flags) return WK_ERR_ARG;
+  *kind = c->ipc ? 3 : c->host_ar ? 2 : c->comm ? 1 : 0;
+  *flags = (c->xch && c->xch_uncached) ? 1 : 0;
+  return WK_OK;
+}
+
 int wk_allreduce_test(wk_ctx* c, float* host_buf, int n) {
   DevGuard dg_(c);
   if (!c || !host_buf || n <= 0) return WK_ERR_ARG;
@@ -1365,10 +1456,7 @@ int wk_allreduce_test(wk_ctx* c, float* host_buf, int n) {
     HIPCHK(c, wk::launch_reduce_xch_adam(x, c->stream));
     HIPCHK(c, hipMemcpyAsync(host_buf, out, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    uint32_t err = 0;
-    HIPCHK(c, hipMemcpy(&err, c->xch_err, sizeof err, hipMemcpyDeviceToHost));
-    if (err) { SETERR(c, "IPC exchange: a peer never published (timeout)"); return WK_ERR_COMM; }
-    return WK_OK;
+    return xch_status(c);
   }
   if (ensure(c, &c->scratch, &c->scratch_bytes, sizeof(float) * n)) return WK_ERR_HIP;
   HIPCHK(c, hipMemcpyAsync(c->scratch, host_buf, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
@@ -1385,7 +1473,7 @@ int wk_count_events(wk_ctx* c, int k, uint64_t* counts) {
   DevGuard dg_(c);
   if (!c || !counts || k <= 0) return WK_ERR_ARG;
   if (k > c->T_valid) { SETERR(c, "count replay of %d env-steps, the trajectory holds %d", k, c->T_valid); return WK_ERR_STATE; }
-  if (c->P.rough || c->scene.n_props > 0) { SETERR(c, "the counting replay runs on the flat floor without props"); return WK_ERR_CONFIG; }
+  if (c->scene.n_props > 0) { SETERR(c, "the counting replay runs without scene props"); return WK_ERR_CONFIG; }
   static_assert(WK_NEV == wk::NEV, "event counters");
   if (!c->counts) HIPCHK(c, hipMalloc((void**)&c->counts, sizeof(unsigned long long) * wk::NEV));
   HIPCHK(c, hipMemsetAsync(c->counts, 0, sizeof(unsigned long long) * wk::NEV, c->stream));

@@ -141,7 +141,12 @@ hipError_t launch_adam(const AdamArgs& a, hipStream_t s);
 // reduction and Adam (wk_comm_init_ipc): rank r's exchange region is [2][SLAB] floats
 // (double-buffered by minibatch parity) then XCH_FLAGS uint64 sequence flags, one per block of
 // the fused kernel (each block owns a span of parameter quads).
-enum : int { XCH_FLAGS = 128, XCH_MAX_RANKS = 8 };
+// XCH_TIMEOUT_TICKS: the bounded wait for a peer's flag, in s_memrealtime ticks (the 100 MHz
+// constant clock): 2 s.  XCH_MAX_RANKS_PER_DEVICE: more ranks sharing one GPU stall (their
+// waiting exchange blocks hold the CUs a peer's gradient kernel needs), so wk_comm_init_ipc
+// refuses them.
+enum : int { XCH_FLAGS = 128, XCH_MAX_RANKS = 8, XCH_MAX_RANKS_PER_DEVICE = 4 };
+constexpr uint64_t XCH_TIMEOUT_TICKS = 200000000ull;
 struct XchArgs {
   const float* partial;                // this rank's gradient-kernel block slabs [nblocks][SLAB]
   int nblocks;
@@ -150,8 +155,9 @@ struct XchArgs {
   uint64_t* flag[XCH_MAX_RANKS];       // every rank's XCH_BLOCKS flags
   int rank, nranks;
   uint64_t seq;                        // this minibatch's sequence number (from 1)
-  uint32_t* err;                       // set to 1 if a peer never published (bounded wait)
-  AdamArgs a;
+  uint32_t* err;                       // set to 1 if a peer never published (bounded wait); once
+                                       // set, every later exchange is a no-op (no Adam)
+  AdamArgs a;                          // a.W == null: exchange only (gradient-only calls)
 };
 size_t xch_region_bytes();
 hipError_t launch_reduce_xch_adam(const XchArgs& x, hipStream_t s);

@@ -703,7 +703,7 @@ DEV bool state_finite(const EnvState& s) {
 // physics with per-lane event counters summed into A.counts (SURVEY 8(d) F_counted).
 template <bool POLICY, bool RECORD, bool TRACE, int L, bool ROUGH, bool COUNT = false>
 __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArgs A) {
-  static_assert(!COUNT || (L == 1 && !POLICY && !TRACE && !ROUGH), "counting replay");
+  static_assert(!COUNT || (L == 1 && !POLICY && !TRACE), "counting replay");
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = tid / L, sub = tid % L;
   const int n = P.n_env;
@@ -1488,10 +1488,11 @@ hipError_t launch_env_scene(int mode, const EnvParams& P, const StepArgs& A, con
   return hipGetLastError();
 }
 hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
-  if (mode == 4) {  // counting replay: one lane per walker, given actions, flat floor
-    if (P.rough || !A.counts || !A.actions) return hipErrorInvalidValue;
+  if (mode == 4) {  // counting replay: one lane per walker, given actions (flat or rough floor)
+    if (!A.counts || !A.actions) return hipErrorInvalidValue;
     dim3 blk(64), grd((unsigned)((P.n_env + 63) / 64));
-    hipLaunchKernelGGL((k_env_step<false, false, false, 1, false, true>), grd, blk, 0, s, P, A);
+    if (P.rough) hipLaunchKernelGGL((k_env_step<false, false, false, 1, true, true>), grd, blk, 0, s, P, A);
+    else hipLaunchKernelGGL((k_env_step<false, false, false, 1, false, true>), grd, blk, 0, s, P, A);
     return hipGetLastError();
   }
   if (P.lanes == 2) (P.rough ? launch_side_pair_rough : launch_side_pair)(mode, P, A, s);

@@ -498,8 +498,17 @@ hipError_t launch_grad_reduce_adam(const float* partial, int nblocks, float* par
 // applies Adam.  A buffer is reused two minibatches later only: a rank publishes seq + 2 after
 // its exchange of seq + 1 saw every peer's seq + 1 flag, which a peer sets only once its own
 // exchange of seq -- the last read of the seq buffers -- has completed (stream order).
+// Failure: the wait is bounded by XCH_TIMEOUT_TICKS of the constant 100 MHz clock (2 s); a block
+// whose wait times out sets *err and returns without writing grad_out or applying Adam, and
+// every later exchange sees *err at entry and returns before publishing (so the peers time out
+// too and the error reaches every rank) -- W / m / v keep their values from the last good
+// minibatch.  (Only a peer that dies half-way through publishing one minibatch's flags can
+// leave that minibatch applied in some blocks and not in others; the job is dead then.)
 __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
   __shared__ float4 gs[RG][QB];
+  __shared__ int live;  // no exchange has timed out (entry), and this block's wait completed
+  if (threadIdx.x == 0)
+    live = __hip_atomic_load(x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u ? 1 : 0;
   const int qi = threadIdx.x % QB, gi = threadIdx.x / QB;
   const int q = blockIdx.x * QB + qi;
   const int ngroups = (x.nblocks + RG - 1) / RG;
@@ -524,6 +533,7 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
   }
   gs[gi][qi] = acc;
   __syncthreads();
+  if (!live) return;  // an earlier exchange timed out (block-uniform: read after the barrier)
   const int buf = (int)(x.seq & 1u);
   float mine = 0.0f;
   if (gi < 4 && q < SLAB / 4) {  // stage 2: this rank's ordered sum, published
@@ -545,19 +555,20 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
   const int t = threadIdx.x;
   if (t == 0)
     __hip_atomic_store(x.flag[x.rank] + blockIdx.x, x.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (t < x.nranks && t != x.rank &&
-      __hip_atomic_load(x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+  if (t < x.nranks && t != x.rank) {
     const uint64_t* f = x.flag[t] + blockIdx.x;
-    uint32_t spins = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < x.seq) {
-      if (++spins > (1u << 26)) {  // seconds: a peer is gone -- report, never hang the GPU (and
-        atomicOr(x.err, 1u);       // the next exchanges skip the wait once this is set)
+      if (__builtin_amdgcn_s_memrealtime() - t0 > XCH_TIMEOUT_TICKS) {
+        atomicOr(x.err, 1u);  // a peer is gone: report, never hang the GPU
+        live = 0;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
   }
   __syncthreads();
+  if (!live) return;  // no grad_out, no Adam: the weights keep the last good minibatch's values
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale peer lines
   if (gi < 4 && q < SLAB / 4) {
     float sum = x.rank == 0 ? mine : x.slab[0][(size_t)buf * SLAB + p];

@@ -18,6 +18,7 @@ NPARAM = 6149
 NPARAM_CRITIC = 897
 NPAIRS = 9
 NEV = 16  # WK_NEV event counters (wk_count_events)
+IPC_HANDLE_BYTES = 128  # WK_IPC_HANDLE_BYTES: IPC handle + the device's PCI bus id
 EVENTS = ["joint", "aabb_ll", "aabb_lf", "aabb_bf", "sat_ll", "sat_lf", "sat_bf", "imp_ll",
           "imp_lf", "imp_bf", "contacts", "substeps", "env_steps", "resets", "steps_lf", "steps_satll"]
 ST_TORQUE, ST_POS, ST_PREV, ST_STEPS, ST_POSTRESET, ST_TERMINAL, ST_EPISODES = (
@@ -40,8 +41,8 @@ EXPORTS = [
     "wk_episode_log_drain", "wk_loss_log_drain", "wk_write_data_file",
     "wk_comm_unique_id", "wk_comm_init", "wk_comm_init_host", "wk_allreduce_test", "wk_profile_enable",
     "wk_profile_get", "wk_profile_reset", "wk_count_events", "wk_snapshot", "wk_time_gradient",
-    "wk_grad_kernel",
-    "wk_comm_ipc_handle", "wk_comm_init_ipc",
+    "wk_time_gradient_ex", "wk_grad_kernel", "wk_rollout_mapping",
+    "wk_comm_ipc_handle", "wk_comm_init_ipc", "wk_comm_info",
 ]
 
 
@@ -235,6 +236,9 @@ def load_library(path=None):
         "wk_allreduce_test": (I, [P, P, I]),
         "wk_comm_init_host": (I, [P, I, I, HOST_ALLREDUCE_FN, P]),
         "wk_time_gradient": (I, [P, I, I, C.POINTER(C.c_double)]),
+        "wk_time_gradient_ex": (I, [P, I, I, I, C.POINTER(C.c_double)]),
+        "wk_rollout_mapping": (I, [P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int64)]),
+        "wk_comm_info": (I, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "wk_grad_kernel": (I, [P, I]),
         "wk_comm_ipc_handle": (I, [P, P]),
         "wk_comm_init_ipc": (I, [P, I, I, P]),
@@ -675,18 +679,45 @@ class Engine:
         self._chk(self.lib.wk_comm_init_host(self.h, int(rank), int(nranks), self._host_ar, None),
                   "wk_comm_init_host")
 
-    def comm_init_ipc(self, rank, nranks, allgather):
-        """wk_comm_ipc_handle + wk_comm_init_ipc: the one-shot exchange over peer-mapped memory.
-        `allgather(bytes) -> list of bytes` (rank order) exchanges the 64-byte IPC handles over
-        any control plane (e.g. torch.distributed.all_gather_object over gloo)."""
-        h = (C.c_uint8 * 64)()
+    def comm_ipc_handle(self):
+        """wk_comm_ipc_handle: this rank's IPC_HANDLE_BYTES exchange record"""
+        h = (C.c_uint8 * IPC_HANDLE_BYTES)()
         self._chk(self.lib.wk_comm_ipc_handle(self.h, h), "wk_comm_ipc_handle")
-        handles = allgather(bytes(h))
-        if len(handles) != nranks or any(len(x) != 64 for x in handles):
-            raise WkError("wk_comm_init_ipc: need one 64-byte handle per rank")
-        buf = (C.c_uint8 * (64 * nranks)).from_buffer_copy(b"".join(handles))
+        return bytes(h)
+
+    def comm_init_ipc_records(self, rank, nranks, records):
+        """wk_comm_init_ipc with every rank's record (rank order)"""
+        if len(records) != nranks or any(len(x) != IPC_HANDLE_BYTES for x in records):
+            raise WkError(f"wk_comm_init_ipc: need one {IPC_HANDLE_BYTES}-byte record per rank")
+        buf = (C.c_uint8 * (IPC_HANDLE_BYTES * nranks)).from_buffer_copy(b"".join(records))
         self._chk(self.lib.wk_comm_init_ipc(self.h, int(rank), int(nranks), buf),
                   "wk_comm_init_ipc")
+
+    def comm_init_ipc(self, rank, nranks, allgather):
+        """wk_comm_ipc_handle + wk_comm_init_ipc: the one-shot exchange over peer-mapped memory.
+        `allgather(bytes) -> list of bytes` (rank order) exchanges the records over any control
+        plane (e.g. torch.distributed.all_gather_object over gloo).  Every rank joins the
+        all-gather even when its own handle failed (it sends b""), so the ranks' collectives
+        stay paired; then every rank raises."""
+        try:
+            rec, why = self.comm_ipc_handle(), None
+        except WkError as ex:
+            rec, why = b"", str(ex)
+        records = allgather(rec)
+        if why is not None:
+            raise WkError(why)
+        bad = [r for r, x in enumerate(records) if len(x) != IPC_HANDLE_BYTES]
+        if bad:
+            raise WkError(f"wk_comm_init_ipc: rank(s) {bad} have no exchange record")
+        self.comm_init_ipc_records(rank, nranks, records)
+
+    COMM_KINDS = {0: "none", 1: "rccl", 2: "host", 3: "ipc"}
+
+    def comm_info(self):
+        """wk_comm_info: (exchange kind, whether the IPC region is uncached device memory)"""
+        k, f = C.c_int(), C.c_int()
+        self._chk(self.lib.wk_comm_info(self.h, C.byref(k), C.byref(f)), "wk_comm_info")
+        return self.COMM_KINDS[k.value], bool(f.value & 1)
 
     def allreduce_test(self, x):
         x = _f32(x).copy()
@@ -703,13 +734,23 @@ class Engine:
         self._chk(k if k < 0 else 0, "wk_grad_kernel")
         return self.GRAD_KERNELS[k]
 
-    def time_gradient(self, minibatch=0, reps=64):
-        """wk_time_gradient: mean ms of the update's gradient kernel over `reps` back-to-back
-        launches on minibatch 0 of the current trajectory"""
+    def time_gradient(self, minibatch=0, reps=64, per_launch_events=False):
+        """wk_time_gradient_ex: mean ms of the update's gradient kernel over `reps` back-to-back
+        launches on minibatch 0 of the current trajectory -- one event pair around the burst,
+        or (per_launch_events) one around every launch, as profile level 2 times the update"""
         ms = C.c_double()
-        self._chk(self.lib.wk_time_gradient(self.h, int(minibatch), int(reps), C.byref(ms)),
-                  "wk_time_gradient")
+        self._chk(self.lib.wk_time_gradient_ex(self.h, int(minibatch), int(reps),
+                                               int(bool(per_launch_events)), C.byref(ms)),
+                  "wk_time_gradient_ex")
         return ms.value
+
+    def rollout_mapping(self):
+        """wk_rollout_mapping: {lanes_per_walker, walkers_per_wave, waves} of a rollout launch"""
+        L, w = C.c_int(), C.c_int()
+        n = C.c_int64()
+        self._chk(self.lib.wk_rollout_mapping(self.h, C.byref(L), C.byref(w), C.byref(n)),
+                  "wk_rollout_mapping")
+        return {"lanes_per_walker": L.value, "walkers_per_wave": w.value, "waves": n.value}
 
     # -- counting replay / snapshots --
     def count_events(self, k):

@@ -95,6 +95,37 @@ def test_count_events_match_oracle_bookkeeping(wk, orc):
         assert ev[k] == ref[k], (k, ev[k], ref[k])
 
 
+def test_count_events_rough_floor(wk, orc):
+    """the counting replay on CreateRoughFloor's terrain (bench.py's rough-floor rooflines): the
+    replay's physics is the rollout's bit for bit, and the classes the oracle's trace keeps on
+    the rough floor (joints, leg-leg pairs, substeps, env-steps, resets) equal its bookkeeping;
+    the segment pairs (untraced) count as leg-floor / torso-floor events"""
+    n, T = 64, 24
+    eng = wk.Engine(n, seed=SEED, Horizon=T, RandomizeStart=1, RoughFloor=1, MaxTimesteps=20)
+    eng.snapshot()
+    eng.rollout(T)
+    tr = eng.get_trajectory(T)
+    after = eng.get_state()
+    eng.restore()
+    ev = dict(zip(wk.EVENTS, eng.count_events(T).tolist()))
+    np.testing.assert_array_equal(eng.get_state(), after)
+    ref = dict.fromkeys(wk.EVENTS, 0)
+    for i in range(n):
+        e = orc.Env(dx=float(orc.env_offset(SEED, i)), rough=(SEED, i), MaxTimesteps=20)
+        for t in range(T):
+            _, _, d, trc = e.step(tr["actions"][t, i], trace=True)
+            ref["joint"] += int((trc["joint_depth"] != 0).sum())
+            ref["aabb_ll"] += int(trc["aabb_hit"][:, LL].sum())
+            ref["sat_ll"] += int(trc["sat_hit"][:, LL].sum())
+            ref["imp_ll"] += int((trc["n_contacts"][:, LL] > 0).sum())
+            ref["substeps"] += len(trc)
+            ref["env_steps"] += 1
+            ref["resets"] += int(d)
+    for k in ("joint", "aabb_ll", "sat_ll", "imp_ll", "substeps", "env_steps", "resets"):
+        assert ev[k] == ref[k], (k, ev[k], ref[k])
+    assert ev["aabb_lf"] > 0 and ev["sat_lf"] > 0 and ev["resets"] > 0
+
+
 def test_snapshot_restore_repeats_an_iteration(wk):
     n, T = 1024, 8
     eng = wk.Engine(n, seed=SEED, Horizon=T, Minibatch=1024, RandomizeStart=1)

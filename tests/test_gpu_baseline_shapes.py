@@ -17,6 +17,10 @@ the bench runs, at the bench's per-GPU sizes, against the oracle:
     minibatches of the 524,288-sample pool, each gradient -> ordered reduction -> Adam,
     against the oracle's sequential Train(Batch) over the same index sequence
     (PPOAgent.cs:147-172, 218-346, 501-540; DenseLayer.cs:125-159).
+  * the headline: 65,536 walkers on one GPU (BASELINE config 4 at N = 1, the metric's line),
+    auto mapping (the lane-pair split), T_h = 64, once on Carpet and once with RandomizeMaterial
+    = 1 (config 5's Ice / Rubber / Carpet): the same bit-exact replay of every walker through
+    the oracle and the same sampler checks;
   * config 3 at its stated shape: 4,096 walkers, T_h = 64, M = 4,096, E = 5.  Rollout
     replayed bit-exactly; the first minibatch's gradient against the oracle and a float64
     restatement; the first epoch (64 Adam steps) and the whole update (320 Adam steps)
@@ -187,6 +191,19 @@ def shard(request, wk, orc):
     eng, ag, tr = _rollout_and_replay(wk, orc, n, T_H, request.param, Minibatch=n,
                                       MinibatchGlobal=65536, Epochs=1)
     yield request.param, eng, ag, tr
+    eng.close()
+
+
+@pytest.mark.parametrize("materials", [0, 1], ids=["carpet", "materials"])
+def test_headline_65536_rollout_T64_bitexact(wk, orc, materials):
+    """the metric's kernel at the metric's size: k_env_side<..., 1> (lane pairs) with the fused
+    matrix-core policy over 65,536 walkers and 64 env-steps, replayed walker by walker through
+    the oracle (states, rewards, dones and final records bit for bit)"""
+    n = 65536
+    eng, ag, tr = _rollout_and_replay(wk, orc, n, T_H, materials, Minibatch=n, Epochs=1)
+    assert eng.rollout_mapping() == {"lanes_per_walker": 2, "walkers_per_wave": 32,
+                                     "waves": n * 2 // 64}
+    _check_policy_outputs(orc, ag, tr, n, T_H)
     eng.close()
 
 

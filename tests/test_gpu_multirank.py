@@ -87,6 +87,8 @@ def test_two_ranks_allreduce(two_rank_runs, mode):
         assert int(r["t1"]) == 1
         assert float(r["cd"]) == np.float32(r0["cd_l"]) + np.float32(r1["cd_l"])
         assert float(r["ad"]) == np.float32(r0["ad_l"]) + np.float32(r1["ad_l"])
+    for r in (r0, r1):  # gradient-only calls are collective: the sum over the ranks
+        np.testing.assert_array_equal(r["g_x"], g_sum)
     np.testing.assert_array_equal(r0["w2"], r1["w2"])
     np.testing.assert_array_equal(r0["w3"], r1["w3"])
     assert int(r0["t3"]) == int(r1["t3"]) == 2 + 2 * 3 * 4
@@ -121,6 +123,30 @@ def test_three_ranks_ipc_rank_order_sum(tmp_path):
         np.testing.assert_array_equal(rs[0][k], rs[1][k], err_msg=k)
         np.testing.assert_array_equal(rs[0][k], rs[2][k], err_msg=k)
     assert int(rs[2]["t3"]) == 2 + 2 * 3 * 4
+
+
+def test_ipc_peer_never_publishes(tmp_path):
+    """rank 1 maps the exchange and then never publishes.  Rank 0's update
+    fails with WK_ERR_COMM after the stated 2-s bound (XCH_TIMEOUT_TICKS of the 100 MHz constant
+    clock; the later minibatches return at once) and applies no Adam step: W, m and v are
+    bit-identical before and after"""
+    r0, _ = _run_two_ranks(tmp_path, "ipc_silent")
+    print(f"failing update took {float(r0['elapsed']):.2f} s: {r0['raised']}")
+    assert "did not publish" in str(r0["raised"])
+    assert 1.5 <= float(r0["elapsed"]) <= 8.0
+    for k in ("w", "m", "v"):
+        np.testing.assert_array_equal(r0[k + "_before"], r0[k + "_after"], err_msg=k)
+
+
+def test_ipc_refuses_more_than_four_ranks_per_gpu(wk):
+    """wk_comm_init_ipc counts the ranks whose record names this rank's GPU and refuses more than
+    four (their waiting exchange blocks would hold the CUs a peer's gradient kernel needs)"""
+    eng = wk.Engine(64, seed=20250905, Horizon=4, Minibatch=64)
+    rec = eng.comm_ipc_handle()
+    assert len(rec) == wk.IPC_HANDLE_BYTES and rec[64:].rstrip(b"\0")  # the PCI bus id
+    with pytest.raises(wk.WkError, match="at most 4 ranks per GPU"):
+        eng.comm_init_ipc_records(0, 5, [rec] * 5)
+    eng.close()
 
 
 def test_failing_host_allreduce_is_reported(wk):

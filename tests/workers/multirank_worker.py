@@ -32,6 +32,36 @@ def allreduce(a):
 
 
 eng = wk.Engine(n_local, seed=SEED, **cfg)
+if mode == "ipc_silent":
+    # rank 1 maps the exchange and then never publishes; rank 0's update must
+    # fail with WK_ERR_COMM within the 2-s bound and leave W / m / v exactly as they were
+    import time
+
+    def allgather(b):
+        out = [None] * world
+        dist.all_gather_object(out, b)
+        return out
+    eng.comm_init_ipc(rank, world, allgather)
+    res = {}
+    if rank == 0:
+        eng.rollout(T)
+        eng.sync()
+        w_before = eng.get_weights()
+        m_before, v_before, _ = eng.get_adam()
+        t0 = time.perf_counter()
+        try:
+            eng.ppo_update(update_index=0)
+            raised = ""
+        except wk.WkError as ex:
+            raised = str(ex)
+        res = dict(elapsed=time.perf_counter() - t0, raised=raised, w_before=w_before,
+                   w_after=eng.get_weights(), m_before=m_before, v_before=v_before,
+                   m_after=eng.get_adam()[0], v_after=eng.get_adam()[1])
+    dist.barrier()  # rank 1 waits here (gloo), publishing nothing, until rank 0 is done
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
+    eng.close()
+    dist.destroy_process_group()
+    sys.exit(0)
 solo = wk.Engine(n_local, seed=SEED, **cfg)  # same shard, no communicator
 if mode == "ipc":
     def allgather(b):
@@ -67,6 +97,11 @@ g_local, cd_l, ad_l, sk = solo.minibatch_gradient(
     flat(tr["returns"], 1)[idx], flat(tr["advantages"], 1)[idx], b_div=shard.minibatch_global)
 w1 = eng.get_weights()
 m1, v1, t1 = eng.get_adam()
+# a gradient-only call is collective on every kind of context: the sum over the ranks
+# (IPC contexts used to return the rank-local sum here)
+g_x, _, _, _ = eng.minibatch_gradient(
+    flat(tr["states"], 12)[idx], flat(tr["actions"], 4)[idx], flat(tr["logp"], 4)[idx],
+    flat(tr["returns"], 1)[idx], flat(tr["advantages"], 1)[idx], b_div=shard.minibatch_global)
 eng.rollout(T)  # a second iteration: the replicas stay identical
 eng.ppo_update(update_index=1)
 w2 = eng.get_weights()
@@ -80,7 +115,7 @@ w3 = eng.get_weights()
 m3, v3, t3 = eng.get_adam()
 np.savez(os.path.join(out_dir, f"rank{rank}.npz"), w0=w0, w1=w1, m1=m1, v1=v1, t1=t1, w2=w2,
          w3=w3, m3=m3, v3=v3, t3=t3,
-         g_local=g_local, cd=cd, ad=ad, cd_l=cd_l, ad_l=ad_l, same_traj=same_traj,
+         g_local=g_local, g_x=g_x, cd=cd, ad=ad, cd_l=cd_l, ad_l=ad_l, same_traj=same_traj,
          same_state=same_state, state=eng.get_state())
 eng.close()
 solo.close()
