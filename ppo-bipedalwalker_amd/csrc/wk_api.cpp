@@ -83,6 +83,8 @@ struct wk_ctx {
   int snap_adam_t = 0; uint32_t snap_rollout_steps = 0; uint64_t snap_loss_count = 0;
   bool snap_valid = false;
   unsigned long long* counts = nullptr;  // [WK_NEV] device (wk_count_events)
+  int32_t* order = nullptr;       // [n] lane order of the split physics kernels (null: identity)
+  uint32_t* order_cnt = nullptr;  // [order_tiles(n)] episode-0 walkers per tile
   // comm
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
@@ -380,6 +382,13 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   ALLOC(x->ep_count, sizeof(uint64_t));
   ALLOC(x->ep_log, sizeof(wk::EpisodeRecDev) * x->ep_cap);
   ALLOC(x->loss_log, sizeof(float) * 2 * x->loss_cap);
+  if (P.lanes == 2 || P.lanes == 4) {  // (WK_ORDER=0: identity lane order, for measurements)
+    const char* o = getenv("WK_ORDER");
+    if (!(o && o[0] == '0')) {
+      ALLOC(x->order, sizeof(int32_t) * n);
+      ALLOC(x->order_cnt, sizeof(uint32_t) * wk::order_tiles((int)n));
+    }
+  }
 #undef ALLOC
   // synthetic randomisation of the initial state (BASELINE.json config 2 / 5)
   std::vector<float> dx(n, 0.0f);
@@ -427,7 +436,7 @@ int wk_destroy(wk_ctx* c) {
   void* bufs[] = {c->st, c->dxoff, c->mat, c->rng_t, c->W, c->Wz, c->m, c->v, c->grad, c->ts, c->ta,
                   c->tlp, c->tr, c->tv, c->tret, c->tadv, c->td, c->partial, c->scratch, c->scratch2,
                   c->ep_acc, c->ep_len, c->ep_scratch, c->ep_rowcnt, c->ep_count, c->ep_log,
-                  c->loss_log, c->props, c->snap, c->counts};
+                  c->loss_log, c->props, c->snap, c->counts, c->order, c->order_cnt};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -479,11 +488,18 @@ int wk_set_offsets(wk_ctx* c, const float* dx) {
   return WK_OK;
 }
 
-// the env-step kernel of the context's mapping; with scene props the one-lane scene kernel
+// the env-step kernel of the context's mapping; with scene props the one-lane scene kernel.
+// The split mappings (lane pairs / quads) first order their lanes: episode-0 walkers first
+// (wk_order.hip; WK_ORDER=0 keeps the identity order, for measurements)
 static hipError_t launch_physics(wk_ctx* c, int mode, wk::StepArgs& A) {
   if (c->scene.n_props > 0) {
     A.props = c->props;
     return wk::launch_env_scene(mode, c->P, A, c->scene, c->stream);
+  }
+  if ((c->P.lanes == 2 || c->P.lanes == 4) && c->order) {
+    const hipError_t e = wk::launch_walker_order(c->st, c->n, c->order_cnt, c->order, c->stream);
+    if (e != hipSuccess) return e;
+    A.order = c->order;
   }
   return wk::launch_env_step(mode, c->P, A, c->stream);
 }

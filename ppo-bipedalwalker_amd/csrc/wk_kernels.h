@@ -59,6 +59,7 @@ struct StepArgs {
   int k_steps;
   float* props;              // scene props [n][SceneDev::pstride] (k_env_scene) or null
   unsigned long long* counts;  // [NEV] event totals (counting replay, mode 4) or null
+  const int32_t* order;      // k_env_side: walker of lane slot s (wk_order.hip) or null (identity)
 };
 
 // scene props (wk_scene.inc): Square / Triangle / Hexagon bodies after the floor, the same
@@ -186,6 +187,10 @@ struct EpisodeArgs {
   EpisodeRecDev* log;
 };
 hipError_t launch_episode_log(const EpisodeArgs& a, hipStream_t s);
+// lane order for k_env_side: episode-0 walkers first, then the post-reset ones (wk_order.hip)
+int order_tiles(int n);
+hipError_t launch_walker_order(const float* st, int n, uint32_t* cnt, int32_t* order,
+                               hipStream_t s);
 int episode_count_cells(int n, int T);
 hipError_t launch_episode_reset(int n, const uint8_t* mask, double* acc, int32_t* len,
                                 hipStream_t s);

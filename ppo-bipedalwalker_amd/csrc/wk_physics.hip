@@ -1172,7 +1172,10 @@ void k_env_side(EnvParams P, StepArgs A) {
   // a partial last wave keeps every lane (the policy's MFMAs need the whole wave):
   // out-of-range lanes replay walker n-1 and never store
   const bool active = eraw < n && (tid & 63) < (wpw << SH);
-  const int e = eraw < n ? eraw : n - 1;
+  // lane slot -> walker (wk_order.hip: episode-0 walkers first, so each wave's walkers visit
+  // their floor pairs in one list order); every index below is the walker's own
+  const int slot = eraw < n ? eraw : n - 1;
+  const int e = A.order ? A.order[slot] : slot;
   const bool leader = side == 0 && half == 0 && active;
   __shared__ float pol_lds[POLICY ? (SIDE_BLOCK / 64) * 768 : 1];
   __shared__ float wz_lds[POLICY ? mf::WEND : 1];  // operand-order weights (41 KB, 2 blocks/CU)

@@ -83,25 +83,22 @@ tr = eng.get_trajectory(T)
 tr_solo = solo.get_trajectory(T)
 same_traj = all(np.array_equal(tr[k], tr_solo[k]) for k in tr)
 same_state = np.array_equal(eng.get_state(), solo.get_state())
-cd, ad = eng.ppo_update(update_index=0)
 # this rank's local gradient of the same (only) minibatch, recomputed by the same kernel
 pool = n_local * T
-key = None
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import orc  # noqa: E402  (checker: the permutation the engine draws its minibatch with)
 key = orc.perm_key(SEED, 0, 0)
 idx = np.array([orc.perm(i, pool, key) for i in range(pool)])
 flat = lambda x, d: x.reshape(pool, d) if d > 1 else x.reshape(pool)
-g_local, cd_l, ad_l, sk = solo.minibatch_gradient(
-    flat(tr["states"], 12)[idx], flat(tr["actions"], 4)[idx], flat(tr["logp"], 4)[idx],
-    flat(tr["returns"], 1)[idx], flat(tr["advantages"], 1)[idx], b_div=shard.minibatch_global)
+mb = (flat(tr["states"], 12)[idx], flat(tr["actions"], 4)[idx], flat(tr["logp"], 4)[idx],
+      flat(tr["returns"], 1)[idx], flat(tr["advantages"], 1)[idx])
+g_local, cd_l, ad_l, sk = solo.minibatch_gradient(*mb, b_div=shard.minibatch_global)
+# a gradient-only call is collective on every kind of context: the sum over the ranks
+# (IPC contexts used to return the rank-local sum here); same weights w0
+g_x, _, _, _ = eng.minibatch_gradient(*mb, b_div=shard.minibatch_global)
+cd, ad = eng.ppo_update(update_index=0)
 w1 = eng.get_weights()
 m1, v1, t1 = eng.get_adam()
-# a gradient-only call is collective on every kind of context: the sum over the ranks
-# (IPC contexts used to return the rank-local sum here)
-g_x, _, _, _ = eng.minibatch_gradient(
-    flat(tr["states"], 12)[idx], flat(tr["actions"], 4)[idx], flat(tr["logp"], 4)[idx],
-    flat(tr["returns"], 1)[idx], flat(tr["advantages"], 1)[idx], b_div=shard.minibatch_global)
 eng.rollout(T)  # a second iteration: the replicas stay identical
 eng.ppo_update(update_index=1)
 w2 = eng.get_weights()
