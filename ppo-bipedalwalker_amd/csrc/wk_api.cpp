@@ -84,7 +84,7 @@ struct wk_ctx {
   bool snap_valid = false;
   unsigned long long* counts = nullptr;  // [WK_NEV] device (wk_count_events)
   int32_t* order = nullptr;       // [n] lane order of the split physics kernels (null: identity)
-  uint32_t* order_cnt = nullptr;  // [order_tiles(n)] episode-0 walkers per tile
+  uint32_t* order_cnt = nullptr;  // [order_cells(n)] episode-0 walkers per tile + swap count
   // comm
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
@@ -385,8 +385,8 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   if (P.lanes == 2 || P.lanes == 4) {  // (WK_ORDER=0: identity lane order, for measurements)
     const char* o = getenv("WK_ORDER");
     if (!(o && o[0] == '0')) {
-      ALLOC(x->order, sizeof(int32_t) * n);
-      ALLOC(x->order_cnt, sizeof(uint32_t) * wk::order_tiles((int)n));
+      ALLOC(x->order, sizeof(int32_t) * 3 * n);  // order, then the swap ranks' scratch
+      ALLOC(x->order_cnt, sizeof(uint32_t) * wk::order_cells((int)n));
     }
   }
 #undef ALLOC
@@ -489,15 +489,20 @@ int wk_set_offsets(wk_ctx* c, const float* dx) {
 }
 
 // the env-step kernel of the context's mapping; with scene props the one-lane scene kernel.
-// The split mappings (lane pairs / quads) first order their lanes: episode-0 walkers first
-// (wk_order.hip; WK_ORDER=0 keeps the identity order, for measurements)
+// The split mappings first order their lanes: episode-0 walkers in the last slots (wk_order.hip;
+// WK_ORDER=0 keeps the identity order, for measurements).  Not the quad mapping on the rough
+// floor: at one wave per SIMD the launch lasts as long as its slowest wave, and there the few
+// long-lived episode-0 walkers (rough-floor episodes end within a few steps) gathered into one
+// wave make it the slowest -- 63 -> 74 ms per rollout at 8,192 walkers (scripts/r04_rough2.sh);
+// on the flat floor the quad mapping gains 2-3 % and the pair mapping 9.5 %
 static hipError_t launch_physics(wk_ctx* c, int mode, wk::StepArgs& A) {
   if (c->scene.n_props > 0) {
     A.props = c->props;
     return wk::launch_env_scene(mode, c->P, A, c->scene, c->stream);
   }
-  if ((c->P.lanes == 2 || c->P.lanes == 4) && c->order) {
-    const hipError_t e = wk::launch_walker_order(c->st, c->n, c->order_cnt, c->order, c->stream);
+  if (c->order && (c->P.lanes == 2 || (c->P.lanes == 4 && !c->P.rough))) {
+    const hipError_t e = wk::launch_walker_order(c->st, c->n, c->order_cnt, c->order, c->order + c->n,
+                                                 c->stream);
     if (e != hipSuccess) return e;
     A.order = c->order;
   }

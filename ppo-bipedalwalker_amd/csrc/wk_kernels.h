@@ -188,9 +188,9 @@ struct EpisodeArgs {
 };
 hipError_t launch_episode_log(const EpisodeArgs& a, hipStream_t s);
 // lane order for k_env_side: episode-0 walkers first, then the post-reset ones (wk_order.hip)
-int order_tiles(int n);
+int order_cells(int n);  // counters: one per tile of 1,024 slots + the swap count
 hipError_t launch_walker_order(const float* st, int n, uint32_t* cnt, int32_t* order,
-                               hipStream_t s);
+                               int32_t* scratch /* [2 n] */, hipStream_t s);
 int episode_count_cells(int n, int T);
 hipError_t launch_episode_reset(int n, const uint8_t* mask, double* acc, int32_t* len,
                                 hipStream_t s);

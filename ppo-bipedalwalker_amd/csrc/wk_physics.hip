@@ -248,7 +248,7 @@ DEV bool sat_split(const Poly<N>& A, const Poly<N>& B, int half, V2& normal, flo
   bool sep = false;
   V2 nn = mk(0.0f, 0.0f);
   float dd = FLT_MAX;
-  axis_pass<N, N, false, false>(P, Q, sep, nn, dd, &AXP);
+  axis_pass<N, N, false, false, N, N == 6>(P, Q, sep, nn, dd, &AXP);  // (P: a walker pole)
   const float dd_o = hswap(dd), nx_o = hswap(nn.x), ny_o = hswap(nn.y);
   const float dA = half ? dd_o : dd, dB = half ? dd : dd_o;
   const V2 nA = half ? mk(nx_o, ny_o) : nn, nB = half ? nn : mk(nx_o, ny_o);
@@ -291,7 +291,7 @@ DEV bool sat_floor_split(const Poly<6>& A, const Poly<4>& F, float mnx, float mn
   V2 nn = mk(0.0f, 0.0f);
   float dd = FLT_MAX;
   EdgeAxes<6> own;
-  axis_pass<6, 4, true, false, 3>(R, F, sep, nn, dd, &own);
+  axis_pass<6, 4, true, false, 3, true>(R, F, sep, nn, dd, &own);  // (R: the pole, maybe rotated by 3)
   const float dd_o = hswap(dd), nx_o = hswap(nn.x), ny_o = hswap(nn.y);
   const float d0 = half ? dd_o : dd, d1 = half ? dd : dd_o;
   const V2 n0 = half ? mk(nx_o, ny_o) : nn, n1 = half ? nn : mk(nx_o, ny_o);
@@ -358,9 +358,11 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   if constexpr (H == 2 && FLAT) hit = sat_floor_split(A, B, mnx, mny, mxx, mxy, sub, n, depth, axa);
   else if constexpr (H == 2) hit = sat_split(A, B, sub, n, depth, own, axa);
   else if constexpr (L > 1) hit = sat_row<L>(A, B, sub, n, depth);
-  else if constexpr (FLAT) hit = sat_floor(A, B, mnx, mny, mxx, mxy, n, depth, &axa);
-  else if constexpr (KEEP) hit = sat<NA, NB, false>(A, B, n, depth, &axa, &axb);
-  else hit = sat<NA, NB, GENERIC>(A, B, n, depth);
+  // (a Poly<6> here is always a walker pole: A is a leg segment or the torso, B a leg segment
+  // or a floor; scene props resolve in wk_scene.inc)
+  else if constexpr (FLAT) hit = sat_floor<NA, NA == 6>(A, B, mnx, mny, mxx, mxy, n, depth, &axa);
+  else if constexpr (KEEP) hit = sat<NA, NB, false, true>(A, B, n, depth, &axa, &axb);
+  else hit = sat<NA, NB, GENERIC, true>(A, B, n, depth);
   rp_mark(rp, RP_SAT);
   DUP(2, { const auto Ap = perturbed(A); V2 n2; float d2;
            const bool h2 = sat(Ap, B, n2, d2); sink(n2.x); sink(n2.y); sink(d2); sink(h2 ? 1.0f : 0.0f); });
@@ -1045,6 +1047,17 @@ DEV bool side_finite(const SideState& s) {  // this side's legs and the torso (s
 // the four lane groups.  fp32 throughout; only the association of the k-sums differs
 // from the sequential reference (parity tests: rtol 1e-5).
 typedef float pf4 __attribute__((ext_vector_type(4)));
+// an opaque copy of a lane value: the address arithmetic built on it is redone where it is used
+// instead of being strength-reduced into per-lane 64-bit pointers that live across a loop
+#ifndef WK_OPAQUE
+#define WK_OPAQUE 1
+#endif
+DEV uint32_t lane_opaque(uint32_t v) {
+#if WK_OPAQUE
+  asm volatile("" : "+v"(v));
+#endif
+  return v;
+}
 DEV void st_nt4(float* p, float a, float b, float c, float d) {
   const pf4 v = {a, b, c, d};
   __builtin_nontemporal_store(v, (pf4*)p);
@@ -1227,13 +1240,17 @@ void k_env_side(EnvParams P, StepArgs A) {
       for (int d = 0; d < 4; d++) mean[d] = tanhf(z3[d]);
       sample_actions(P, A.lp_const, gid, t, mean, a, lp);
       if (RECORD && leader) {  // streamed rows: 16-byte non-temporal stores keep the L2 for Wz
-        const size_t idx = (size_t)(A.t0 + k) * n + e;
+        // row base (uniform, SGPRs) + the lane's 32-bit offset (global_store saddr form): no
+        // per-lane 64-bit pointer per array stays live across the env-step loop (they spilled)
+        const size_t row = (size_t)(A.t0 + k) * n;
+        const uint32_t eo = lane_opaque((uint32_t)e);
 #pragma unroll
         for (int q = 0; q < 3; q++)
-          st_nt4(A.traj_s + idx * 12 + 4 * q, obs[4 * q], obs[4 * q + 1], obs[4 * q + 2], obs[4 * q + 3]);
-        st_nt4(A.traj_a + idx * 4, a[0], a[1], a[2], a[3]);
-        st_nt4(A.traj_lp + idx * 4, lp[0], lp[1], lp[2], lp[3]);
-        __builtin_nontemporal_store(v, A.traj_v + idx);
+          st_nt4(A.traj_s + row * 12 + (eo * 12u + 4u * q), obs[4 * q], obs[4 * q + 1], obs[4 * q + 2],
+                 obs[4 * q + 3]);
+        st_nt4(A.traj_a + row * 4 + eo * 4u, a[0], a[1], a[2], a[3]);
+        st_nt4(A.traj_lp + row * 4 + eo * 4u, lp[0], lp[1], lp[2], lp[3]);
+        __builtin_nontemporal_store(v, A.traj_v + row + eo);
       }
     } else {
 #pragma unroll
@@ -1272,9 +1289,11 @@ void k_env_side(EnvParams P, StepArgs A) {
       terminal = true;
     }
     if (!side_finite(s)) fault |= 1u;
+    const size_t krow = (size_t)k * n;  // (uniform) + the lane's 32-bit offset, as above
+    const uint32_t eo = lane_opaque((uint32_t)e);
     if (A.pos_out && leader) {
-      A.pos_out[((size_t)k * n + e) * 2] = s.posx;
-      A.pos_out[((size_t)k * n + e) * 2 + 1] = s.posy;
+      A.pos_out[krow * 2 + eo * 2u] = s.posx;
+      A.pos_out[krow * 2 + (eo * 2u + 1u)] = s.posy;
     }
     if (terminal) {
       int ep = s.episodes + 1;
@@ -1286,21 +1305,21 @@ void k_env_side(EnvParams P, StepArgs A) {
       get_obs_side(s, side, obs);
       if (leader) {
 #pragma unroll
-        for (int i = 0; i < 12; i++) A.obs_out[((size_t)k * n + e) * 12 + i] = obs[i];
+        for (int i = 0; i < 12; i++) A.obs_out[krow * 12 + (eo * 12u + i)] = obs[i];
       }
     }
     if (leader) {
-      if (A.rew_out) A.rew_out[(size_t)k * n + e] = reward;
-      if (A.done_out) A.done_out[(size_t)k * n + e] = terminal ? 1 : 0;
+      if (A.rew_out) A.rew_out[krow + eo] = reward;
+      if (A.done_out) A.done_out[krow + eo] = terminal ? 1 : 0;
       if (RECORD) {
-        const size_t idx = (size_t)(A.t0 + k) * n + e;
-        __builtin_nontemporal_store(reward, A.traj_r + idx);
-        __builtin_nontemporal_store((uint8_t)(terminal ? 1 : 0), A.traj_d + idx);
+        const size_t row = (size_t)(A.t0 + k) * n;
+        __builtin_nontemporal_store(reward, A.traj_r + row + eo);
+        __builtin_nontemporal_store((uint8_t)(terminal ? 1 : 0), A.traj_d + row + eo);
       }
     }
     t++;
   }
-  if (active && half == 0) store_side(s, A.st, e, side);
+  if (active && half == 0) store_side(s, A.st, lane_opaque((uint32_t)e), side);
 #ifdef WK_REGION_PROF
   if ((threadIdx.x & 63) == 0)
     for (int r = 0; r < 8; r++) atomicAdd(&g_region_prof[r], (unsigned long long)rpv.acc[r]);
