@@ -601,6 +601,44 @@ DEV void significant_face_ax(const Poly<N>& P, const EdgeAxes<N>& AX, V2 n, V2& 
   fmax = sig;
   fdir = first ? vneg(before) : after;
 }
+// significant_face_ax through LDS (the pair mapping's contact faces): instead of carrying the
+// vertex, both neighbours and two axes through ten bit-select chains over the N vertices, the
+// lane writes its polygon and axes as N float4 records (x, y, axis x, axis y) into its own LDS
+// column rec[k * S] (S: the block's lanes, so a wave's 16-byte accesses hit distinct banks), finds
+// the first strict minimum's index, and reads the three records it needs.  The same index rule as
+// significant_face_ax: with no projection below MaxValue (index -1) the vertex is Vector2.Zero,
+// its neighbours are vertices 0 and N - 2 and its axes N - 1 and N - 2 (the wrapped indices).
+template <int N, int S>
+DEV void significant_face_lds(const Poly<N>& P, const EdgeAxes<N>& AX, V2 n, float4* rec, V2& fa,
+                              V2& fb, V2& fmax, V2& fdir) {
+#pragma unroll
+  for (int k = 0; k < N; k++) rec[k * S] = make_float4(P.x[k], P.y[k], AX.x[k], AX.y[k]);
+  float mind = FLT_MAX;
+  int idx = -1;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const float p = P.x[i] * n.x + P.y[i] * n.y;
+    const bool lt = p < mind;
+    mind = lt ? p : mind;
+    idx = lt ? i : idx;
+  }
+  const int ie = idx < 0 ? N - 1 : idx;           // axis i (-1 wraps to N - 1)
+  const int inx = idx == N - 1 ? 0 : idx + 1;      // vertex i + 1 (-1 -> 0)
+  const int ipv = idx <= 0 ? idx + N - 1 : idx - 1;  // vertex and axis i - 1 (-1 -> N - 2)
+  __builtin_amdgcn_wave_barrier();  // (the lane reads only its own column: no other lane's data)
+  const float4 re = rec[ie * S], rn = rec[inx * S], rp = rec[ipv * S];
+  const V2 sig = idx < 0 ? mk(0.0f, 0.0f) : mk(re.x, re.y);
+  const V2 va = mk(rn.x, rn.y);
+  const V2 vb = mk(rp.x, rp.y);
+  const V2 after = mk(-re.w, re.z);    // -(axis_i.y, -axis_i.x)
+  const V2 before = mk(rp.w, -rp.z);   // (axis_{i-1}.y, -axis_{i-1}.x)
+  const bool first = vdot(n, before) >= vdot(n, after);
+  fa = first ? sig : va;
+  fb = first ? vb : sig;
+  fmax = sig;
+  fdir = first ? vneg(before) : after;
+}
+
 // the flat floor's normalised edges (Environment.cs:219-223): (0,-150), (1100,0), (0,150),
 // (-1100,0) normalise to exactly (+0,-1), (1,+0), (+0,1), (-1,+0); as axes (-ey, ex) * val
 DEV EdgeAxes<4> floor_axes() {
@@ -661,12 +699,19 @@ DEV int contact_clip(V2 ra, V2 rb, V2 rmax, V2 rd, V2 ia, V2 ib, V2 imax, V2 id,
   return cnt;
 }
 // GetContactPoints with both polygons' SAT axes kept: the faces' directions come normalised
-template <int NA, int NB>
+template <int NA, int NB, int S = 0>  // S > 0: both faces through LDS (one column, in turn)
 DEV int contact_points_ax(const Poly<NA>& A, const EdgeAxes<NA>& AXA, const Poly<NB>& B,
-                          const EdgeAxes<NB>& AXB, V2 normal, V2& c0, V2& c1) {
+                          const EdgeAxes<NB>& AXB, V2 normal, V2& c0, V2& c1,
+                          float4* rec = nullptr) {
   V2 ra, rb, rmax, rd, ia, ib, imax, id;
-  significant_face_ax(A, AXA, normal, ra, rb, rmax, rd);
-  significant_face_ax(B, AXB, vneg(normal), ia, ib, imax, id);
+  if constexpr (S > 0) {
+    significant_face_lds<NA, S>(A, AXA, normal, rec, ra, rb, rmax, rd);
+    __builtin_amdgcn_wave_barrier();  // (A's records read before B's overwrite them: same lane)
+    significant_face_lds<NB, S>(B, AXB, vneg(normal), rec, ia, ib, imax, id);
+  } else {
+    significant_face_ax(A, AXA, normal, ra, rb, rmax, rd);
+    significant_face_ax(B, AXB, vneg(normal), ia, ib, imax, id);
+  }
   return contact_clip(ra, rb, rmax, rd, ia, ib, imax, id, normal, c0, c1);
 }
 // significant_face_ax(floor_poly, floor_axes(), n) for the flat floor box, vertices
@@ -700,11 +745,12 @@ DEV void floor_face_ax(V2 n, V2& fa, V2& fb, V2& fmax, V2& fdir) {
   fmax = sig;
   fdir = first ? vneg(before) : after;
 }
-template <int NA>
+template <int NA, int S = 0>  // S > 0: A's face through LDS (significant_face_lds, column rec)
 DEV int contact_points_floor(const Poly<NA>& A, const EdgeAxes<NA>& AXA, V2 normal, V2& c0,
-                             V2& c1) {
+                             V2& c1, float4* rec = nullptr) {
   V2 ra, rb, rmax, rd, ia, ib, imax, id;
-  significant_face_ax(A, AXA, normal, ra, rb, rmax, rd);
+  if constexpr (S > 0) significant_face_lds<NA, S>(A, AXA, normal, rec, ra, rb, rmax, rd);
+  else significant_face_ax(A, AXA, normal, ra, rb, rmax, rd);
 #if WK_FLOOR_FACE_LOOP
   Poly<4> F;
   floor_poly(F);

@@ -321,10 +321,11 @@ DEV bool sat_floor_split(const Poly<6>& A, const Poly<4>& F, float mnx, float mn
 // contact faces are evaluated in general, with Vector2.Normalize's NaN for a zero edge.
 // H = 2: the quad mapping (sub = this lane's half): SAT axes and contact faces split over
 // the leg's two lanes (leg-leg and leg-floor pairs of Poly<6> segments).
-template <int NA, int NB, bool BSTATIC, bool TRACE, int L, bool GENERIC = false, int H = 1>
+// FS > 0: the contact faces through this lane's LDS column frec (stride FS, the pair mapping)
+template <int NA, int NB, bool BSTATIC, bool TRACE, int L, bool GENERIC = false, int H = 1, int FS = 0>
 DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB,
                       bool& colA, PairTraceDev* tr, int pi, int sub, RegionProf* rp = nullptr,
-                      uint32_t* ec = nullptr) {
+                      uint32_t* ec = nullptr, float4* frec = nullptr) {
   static_assert(H == 1 || (L == 1 && !GENERIC && NA == 6 && NB == (BSTATIC ? 4 : 6)),
                 "the quad split covers leg-leg and leg-floor pairs");
   static_assert(!BSTATIC || NB == 4, "the static body is the floor");
@@ -371,8 +372,8 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   V2 c0, c1;
   int nc;
   if constexpr (H == 2 && !BSTATIC) nc = contacts_split(own, axa, sub, n, c0, c1);
-  else if constexpr (KEEP && FLAT) nc = contact_points_floor(A, axa, n, c0, c1);
-  else if constexpr (KEEP) nc = contact_points_ax(A, axa, B, axb, n, c0, c1);
+  else if constexpr (KEEP && FLAT) nc = contact_points_floor<NA, FS>(A, axa, n, c0, c1, frec);
+  else if constexpr (KEEP) nc = contact_points_ax<NA, NB, FS>(A, axa, B, axb, n, c0, c1, frec);
   else nc = contact_points<NA, NB, GENERIC>(A, B, n, c0, c1);
   rp_mark(rp, RP_CONTACT);
   DUP(3, { const auto Ap = perturbed(A); V2 e0, e1;
@@ -977,9 +978,10 @@ DEV void get_obs_side(const SideState& s, int side, float o[12]) {
 // ROUGH: the floor candidates are CreateRoughFloor's 10 segments (floor_pairs, general SAT /
 // contacts, replicated in both halves of the quad mapping; ter: this walker's terrain column in
 // LDS with stride TS); the leg-leg pairs keep their split
-template <bool TRACE, int Q, bool ROUGH = false, int TS = 1>
+template <bool TRACE, int Q, bool ROUGH = false, int TS = 1, int FS = 0>
 DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
-                      PairTraceDev* tr, int side, int half, RegionProf* rp, const float* ter = nullptr) {
+                      PairTraceDev* tr, int side, int half, RegionProf* rp, const float* ter = nullptr,
+                      float4* frec = nullptr) {
   rp_mark(rp, RP_OTHER);
   Poly<4> fl;
   floor_poly(fl);
@@ -1006,10 +1008,10 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
            sink(l2.x[0]); sink(l2.y[5]); sink(d2.th); });
 #pragma unroll
   for (int q = 0; q < 3; q++) {  // [floor if post], other segment, [floor if episode 0]
-    if (q == 1) resolve_pair<6, 6, false, TRACE, 1, false, Q>(s.lo, s.dlo, mp, s.up, s.dup, mp, s.clo, tr, pb + 0, half, rp);
+    if (q == 1) resolve_pair<6, 6, false, TRACE, 1, false, Q, FS>(s.lo, s.dlo, mp, s.up, s.dup, mp, s.clo, tr, pb + 0, half, rp, nullptr, frec);
     else if ((q == 0) == s.post) {
       if constexpr (ROUGH) floor_pairs<6, TRACE, 1, true, TS>(s.lo, s.dlo, mp, s.clo, tr, pb + 1, 0, ter);
-      else resolve_pair<6, 4, true, TRACE, 1, false, Q>(s.lo, s.dlo, mp, fl, dfl, mf, s.clo, tr, pb + 1, half, rp);
+      else resolve_pair<6, 4, true, TRACE, 1, false, Q, FS>(s.lo, s.dlo, mp, fl, dfl, mf, s.clo, tr, pb + 1, half, rp, nullptr, frec);
     }
     rp_mark(rp, RP_OTHER);
   }
@@ -1017,10 +1019,10 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
   rp_mark(rp, RP_INTEG);
 #pragma unroll
   for (int q = 0; q < 3; q++) {
-    if (q == 1) resolve_pair<6, 6, false, TRACE, 1, false, Q>(s.up, s.dup, mp, s.lo, s.dlo, mp, s.cup, tr, pb + 2, half, rp);
+    if (q == 1) resolve_pair<6, 6, false, TRACE, 1, false, Q, FS>(s.up, s.dup, mp, s.lo, s.dlo, mp, s.cup, tr, pb + 2, half, rp, nullptr, frec);
     else if ((q == 0) == s.post) {
       if constexpr (ROUGH) floor_pairs<6, TRACE, 1, true, TS>(s.up, s.dup, mp, s.cup, tr, pb + 3, 0, ter);
-      else resolve_pair<6, 4, true, TRACE, 1, false, Q>(s.up, s.dup, mp, fl, dfl, mf, s.cup, tr, pb + 3, half, rp);
+      else resolve_pair<6, 4, true, TRACE, 1, false, Q, FS>(s.up, s.dup, mp, fl, dfl, mf, s.cup, tr, pb + 3, half, rp, nullptr, frec);
     }
     rp_mark(rp, RP_OTHER);
   }
@@ -1157,6 +1159,9 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool wri
   wave_lds_sync();  // outputs read before the next env-step rewrites the tile
 }
 
+#ifndef WK_FACE_LDS
+#define WK_FACE_LDS 1  // the pair mapping's contact faces through LDS (significant_face_lds)
+#endif
 #ifndef WK_QUAD_WAVES
 #define WK_QUAD_WAVES 1  // waves per SIMD the quad mapping is built for
 #endif
@@ -1196,6 +1201,12 @@ void k_env_side(EnvParams P, StepArgs A) {
   // [draw][walker of block]; the walker's lanes write the same values and read only its column
   constexpr int WPB = SIDE_BLOCK >> SH;
   __shared__ float ter_lds[ROUGH ? 11 * WPB : 1];
+  // the pair mapping's contact faces (significant_face_lds): 6 float4 records per lane,
+  // [record][lane of block] (24 KB per block; 2 blocks of 77 KB fit a CU's 160 KB -- not with the
+  // rough floor's terrain as well, which would leave one block per CU)
+  constexpr int FS = (Q == 1 && !ROUGH && WK_FACE_LDS) ? SIDE_BLOCK : 0;
+  __shared__ float4 face_lds[FS ? 6 * SIDE_BLOCK : 1];
+  float4* const frec = face_lds + (FS ? threadIdx.x : 0);
   const int wib = ((threadIdx.x >> 6) * wpw) + ((threadIdx.x & ((wpw << SH) - 1)) >> SH);
   const float* const ter = ter_lds + wib;
   if constexpr (ROUGH) {
@@ -1267,7 +1278,7 @@ void k_env_side(EnvParams P, StepArgs A) {
 #pragma unroll 1
     for (int it = 0; it < P.iterations; it++) {
       PairTraceDev* tr = (TRACE && active && half == 0) ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
-      substep_side<TRACE, Q, ROUGH, WPB>(s, mp, mb, dt, adx, ady, tr, side, half, rp, ter);
+      substep_side<TRACE, Q, ROUGH, WPB, FS>(s, mp, mb, dt, adx, ady, tr, side, half, rp, ter, frec);
     }
     // Walker.Update + terminal flags (both upper legs and the torso)
     s.prevx = s.posx; s.prevy = s.posy;
