@@ -261,11 +261,12 @@ DEV bool sat_split(const Poly<N>& A, const Poly<N>& B, int half, V2& normal, flo
 }
 // GetContactPoints with the two faces split: half 0 A's on the normal, half 1 B's on its
 // negation (each from its own SAT axes), exchanged, then the clipping in both
-template <int N>
+template <int N, int FS = 0>  // FS > 0: the face through LDS (significant_face_lds, column frec)
 DEV int contacts_split(const Poly<N>& P, const EdgeAxes<N>& AXP, int half, V2 normal, V2& c0,
-                       V2& c1) {
+                       V2& c1, float4* frec = nullptr) {
   V2 fa, fb, fm, fd;
-  significant_face_ax(P, AXP, half ? vneg(normal) : normal, fa, fb, fm, fd);
+  if constexpr (FS > 0) significant_face_lds<N, FS>(P, AXP, half ? vneg(normal) : normal, frec, fa, fb, fm, fd);
+  else significant_face_ax(P, AXP, half ? vneg(normal) : normal, fa, fb, fm, fd);
   const V2 oa = mk(hswap(fa.x), hswap(fa.y)), ob = mk(hswap(fb.x), hswap(fb.y));
   const V2 om = mk(hswap(fm.x), hswap(fm.y)), od = mk(hswap(fd.x), hswap(fd.y));
   const bool h = half != 0;
@@ -371,7 +372,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   if (ec) ec[EV_SAT_LL + EVK]++;
   V2 c0, c1;
   int nc;
-  if constexpr (H == 2 && !BSTATIC) nc = contacts_split(own, axa, sub, n, c0, c1);
+  if constexpr (H == 2 && !BSTATIC) nc = contacts_split<NA, FS>(own, axa, sub, n, c0, c1, frec);
   else if constexpr (KEEP && FLAT) nc = contact_points_floor<NA, FS>(A, axa, n, c0, c1, frec);
   else if constexpr (KEEP) nc = contact_points_ax<NA, NB, FS>(A, axa, B, axb, n, c0, c1, frec);
   else nc = contact_points<NA, NB, GENERIC>(A, B, n, c0, c1);
@@ -1162,6 +1163,9 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool wri
 #ifndef WK_FACE_LDS
 #define WK_FACE_LDS 1  // the pair mapping's contact faces through LDS (significant_face_lds)
 #endif
+#ifndef WK_FACE_LDS_QUAD
+#define WK_FACE_LDS_QUAD 1  // ... and the quad mapping's (one block per CU: its 80 KB fit)
+#endif
 #ifndef WK_QUAD_WAVES
 #define WK_QUAD_WAVES 1  // waves per SIMD the quad mapping is built for
 #endif
@@ -1204,7 +1208,7 @@ void k_env_side(EnvParams P, StepArgs A) {
   // the pair mapping's contact faces (significant_face_lds): 6 float4 records per lane,
   // [record][lane of block] (24 KB per block; 2 blocks of 77 KB fit a CU's 160 KB -- not with the
   // rough floor's terrain as well, which would leave one block per CU)
-  constexpr int FS = (Q == 1 && !ROUGH && WK_FACE_LDS) ? SIDE_BLOCK : 0;
+  constexpr int FS = ((Q == 1 && !ROUGH) || (Q == 2 && WK_FACE_LDS_QUAD)) && WK_FACE_LDS ? SIDE_BLOCK : 0;
   __shared__ float4 face_lds[FS ? 6 * SIDE_BLOCK : 1];
   float4* const frec = face_lds + (FS ? threadIdx.x : 0);
   const int wib = ((threadIdx.x >> 6) * wpw) + ((threadIdx.x & ((wpw << SH) - 1)) >> SH);
