@@ -1164,7 +1164,7 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool wri
 #define WK_FACE_LDS 1  // the pair mapping's contact faces through LDS (significant_face_lds)
 #endif
 #ifndef WK_FACE_LDS_QUAD
-#define WK_FACE_LDS_QUAD 1  // ... and the quad mapping's (one block per CU: its 80 KB fit)
+#define WK_FACE_LDS_QUAD 0  // ... and the quad mapping's (one block per CU: its 80 KB fit; off by default)
 #endif
 #ifndef WK_QUAD_WAVES
 #define WK_QUAD_WAVES 1  // waves per SIMD the quad mapping is built for
