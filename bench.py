@@ -58,7 +58,8 @@ FLOP_SAT = {"ll": 571, "lf": 417, "bf": 349}       # (VA+VB)(11+3(VA+VB))+7, per
 FLOP_CONTACT = {"ll": 190, "lf": 166, "bf": 161}   # contact clipping + MoveObjects, per SAT hit
 FLOP_IMPULSE = 110            # normal + friction impulse pair, per resolution with contacts
 FLOP_POLICY = 10504 + 1793 + 130  # actor + critic forward, sampling / log-prob, obs / reward
-FLOP_UPPER = 3.0e5            # SURVEY's all-pairs-colliding upper bound per env-step
+FLOP_UPPER = 3.0e5            # SURVEY's all-pairs-colliding upper bound per env-step (flat floor:
+                              # the rough floor's 11 segments give the counted F more pairs than it)
 # algorithmic HBM bytes per env-step of the rollout: trajectory row 89 B +
 # the 448-B walker record read and written once per T_h = 64 env-steps
 def alg_bytes_per_env_step(horizon):
@@ -298,7 +299,7 @@ def rollout_roofline(eng, wk, launch_ms, units, horizon, policy=True, traffic=No
         "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
         "peak_no_fma": ceiling, "frac_no_fma": achieved / ceiling, "peak_no_fma_basis": why,
         "mapping": mp,
-        "flop_per_env_step_counted": f, "flop_per_env_step_upper_bound": FLOP_UPPER,
+        "flop_per_env_step_counted": f, "flop_per_env_step_upper_bound_flat_floor": FLOP_UPPER,
         "events_per_env_step": {k: v / ev["env_steps"] for k, v in ev.items() if k != "env_steps"},
         "env_steps_per_launch": units, "mean_launch_ms": launch_ms,
         "hbm_GBs": (traffic / (launch_ms * 1e-3) / 1e9) if traffic else None,

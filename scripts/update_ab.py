@@ -4,6 +4,7 @@ trajectory (restore -> update; one HIP-event pair per update).  The library is w
 names (run once per build).  Prints ms per update and us per minibatch.
 
   WK_LIB=.../libwk.so python scripts/update_ab.py [reps]
+  UPDATE_SHAPES="32768:32768:65536,16384:16384:65536" selects other (walkers:M:M_global) shapes
 """
 import os
 import sys
@@ -14,7 +15,10 @@ import wk  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 T, E = 64, 5
-for n, M, Mg in ((65536, 65536, 65536), (8192, 8192, 65536), (4096, 4096, 4096)):
+SHAPES = ((65536, 65536, 65536), (8192, 8192, 65536), (4096, 4096, 4096))
+if os.environ.get("UPDATE_SHAPES"):
+    SHAPES = tuple(tuple(int(v) for v in sh.split(":")) for sh in os.environ["UPDATE_SHAPES"].split(","))
+for n, M, Mg in SHAPES:
     eng = wk.Engine(n, seed=20250905, Horizon=T, Minibatch=M, MinibatchGlobal=Mg, Epochs=E,
                     RandomizeStart=1)
     for it in range(2):
