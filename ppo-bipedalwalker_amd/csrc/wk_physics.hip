@@ -886,6 +886,28 @@ struct SideState {
   bool post, terminal;
 };
 
+// the legs' 24 vertex coordinates to / from a lane's float4 column (stride FS); see k_env_side
+template <int FS>
+DEV void park_legs(const SideState& s, float4* r) {
+  r[0 * FS] = make_float4(s.lo.x[0], s.lo.x[1], s.lo.x[2], s.lo.x[3]);
+  r[1 * FS] = make_float4(s.lo.x[4], s.lo.x[5], s.lo.y[0], s.lo.y[1]);
+  r[2 * FS] = make_float4(s.lo.y[2], s.lo.y[3], s.lo.y[4], s.lo.y[5]);
+  r[3 * FS] = make_float4(s.up.x[0], s.up.x[1], s.up.x[2], s.up.x[3]);
+  r[4 * FS] = make_float4(s.up.x[4], s.up.x[5], s.up.y[0], s.up.y[1]);
+  r[5 * FS] = make_float4(s.up.y[2], s.up.y[3], s.up.y[4], s.up.y[5]);
+}
+template <int FS>
+DEV void unpark_legs(SideState& s, const float4* r) {
+  float4 a = r[0 * FS], b = r[1 * FS], c = r[2 * FS];
+  s.lo.x[0] = a.x; s.lo.x[1] = a.y; s.lo.x[2] = a.z; s.lo.x[3] = a.w;
+  s.lo.x[4] = b.x; s.lo.x[5] = b.y; s.lo.y[0] = b.z; s.lo.y[1] = b.w;
+  s.lo.y[2] = c.x; s.lo.y[3] = c.y; s.lo.y[4] = c.z; s.lo.y[5] = c.w;
+  a = r[3 * FS]; b = r[4 * FS]; c = r[5 * FS];
+  s.up.x[0] = a.x; s.up.x[1] = a.y; s.up.x[2] = a.z; s.up.x[3] = a.w;
+  s.up.x[4] = b.x; s.up.x[5] = b.y; s.up.y[0] = b.z; s.up.y[1] = b.w;
+  s.up.y[2] = c.x; s.up.y[3] = c.y; s.up.y[4] = c.z; s.up.y[5] = c.w;
+}
+
 template <int CTRL>
 DEV float dppc(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
@@ -1166,6 +1188,9 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool wri
 #ifndef WK_FACE_LDS_QUAD
 #define WK_FACE_LDS_QUAD 0  // ... and the quad mapping's (one block per CU: its 80 KB fit; off by default)
 #endif
+#ifndef WK_POLICY_STASH
+#define WK_POLICY_STASH 1  // the legs' vertices parked in the lane's face column over the policy
+#endif
 #ifndef WK_QUAD_WAVES
 #define WK_QUAD_WAVES 1  // waves per SIMD the quad mapping is built for
 #endif
@@ -1249,6 +1274,15 @@ void k_env_side(EnvParams P, StepArgs A) {
     rp_mark(rp, RP_OTHER);
     if (POLICY) {
       get_obs_side(s, side, obs);
+      // The policy's matrix-core section needs the most registers of the loop, while the legs'
+      // 24 vertex coordinates wait unused until the substeps: park them in this lane's contact-
+      // face column (free outside the contact clipping) rather than leave them to the spill; the
+      // empty asm with a memory clobber keeps the compiler from forwarding the parked values in
+      // registers across the section.  Pure data movement: bit-identical.
+      if constexpr (FS != 0 && WK_POLICY_STASH) {
+        park_legs<FS>(s, frec);
+        asm volatile("" ::: "memory");
+      }
       float z3[4], mean[4], v;
       policy_mfma<Q>(wz_lds, obs, side == 0 && half == 0, wave_pol, z3, v);
 #pragma unroll
@@ -1266,6 +1300,10 @@ void k_env_side(EnvParams P, StepArgs A) {
         st_nt4(A.traj_a + row * 4 + eo * 4u, a[0], a[1], a[2], a[3]);
         st_nt4(A.traj_lp + row * 4 + eo * 4u, lp[0], lp[1], lp[2], lp[3]);
         __builtin_nontemporal_store(v, A.traj_v + row + eo);
+      }
+      if constexpr (FS != 0 && WK_POLICY_STASH) {
+        asm volatile("" ::: "memory");
+        unpark_legs<FS>(s, frec);
       }
     } else {
 #pragma unroll
