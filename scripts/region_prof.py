@@ -1,5 +1,7 @@
 """Per-region wave time of the side-split env-step kernel (build: make LIB=libwk_prof.so
-BUILD=build_prof EXTRA=-DWK_REGION_PROF).  python scripts/region_prof.py [walkers] [T] [lanes]"""
+BUILD=build_prof EXTRA=-DWK_REGION_PROF).  python scripts/region_prof.py [walkers] [T] [lanes]
+REGIME_ITERS=k first runs k PPO iterations at T_h = 64 (the bench's regime protocol), so the
+profiled launches see the walker mix of the timed iteration rather than the seeded start."""
 import ctypes as C
 import os
 import sys
@@ -13,7 +15,11 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 L = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 names = ["joint", "integrate", "aabb", "sat", "contact", "impulse+move", "policy", "other"]
-eng = wk.Engine(n, seed=20250905, Horizon=T, RandomizeStart=1, LanesPerWalker=L)
+R = int(os.environ.get("REGIME_ITERS", "0"))
+eng = wk.Engine(n, seed=20250905, Horizon=max(T, 64 if R else T), RandomizeStart=1, LanesPerWalker=L)
+for it in range(R):
+    eng.rollout(64)
+    eng.ppo_update(update_index=it, sync=False)
 lib = eng.lib
 lib.wk_region_prof.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 buf = (C.c_ulonglong * 16)()
