@@ -102,6 +102,9 @@ def parse():
                         "checked bit for bit against a rank-order reference before timing, and "
                         "RCCL on every rank if the mapping, the test round or the check fails), "
                         "or the RCCL all-reduce")
+    p.add_argument("--detail-file", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                   help="full result (every roofline field, event rates, notes); the stdout line "
+                        "is the compact <= 4 KB summary and names this file ('' = do not write)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_physics.json"))
     return p.parse_args()
 
@@ -269,7 +272,7 @@ def flops_per_env_step(ev, policy=True):
 def valu_ceiling_of(mapping):
     """the non-FMA VALU ceiling of a rollout launch from its real grid (wk_rollout_mapping):
     >= 2 waves per SIMD -> 78.6 T; else one wave per SIMD on the share of SIMDs holding one"""
-    waves = mapping["waves"]
+    waves = mapping.get("waves_launched", mapping["waves"])  # idle waves of the last block run too
     if waves >= 2 * N_SIMDS:
         return PEAK_NOFMA, "scalar non-FMA fp32 issue, >= 2 waves per SIMD"
     return (PEAK_NOFMA_ONE_WAVE * min(1.0, waves / N_SIMDS),
@@ -403,6 +406,112 @@ def extra_config(wk, torch, args, n, M, M_global, horizon, physics_only=False, m
         eng.close()
 
 
+LINE_LIMIT = 4096  # the driver parses one stdout line; round 4's 20 KB line was lost
+
+
+def _r(x, nd=4):
+    """round a float to nd significant digits for the compact line (ints / None unchanged)"""
+    if isinstance(x, float):
+        return float(f"{x:.{nd}g}")
+    return x
+
+
+def _trim_roofline(rf):
+    keep = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "peak_no_fma",
+            "frac_no_fma", "flop_per_env_step_counted", "mean_launch_ms", "hbm_GBs")
+    out = {k: _r(rf[k]) for k in keep if k in rf}
+    if "mapping" in rf:
+        m = rf["mapping"]
+        out["mapping"] = [m.get("lanes_per_walker"), m.get("walkers_per_wave"),
+                          m.get("waves_launched", m.get("waves"))]
+    return out
+
+
+def _trim_update(ru):
+    keep = ("kernel", "achieved", "peak", "unit", "frac", "mean_launch_us",
+            "reduce_adam_us", "reduce_exchange_adam_us", "allreduce_us", "adam_us")
+    out = {k: _r(ru[k]) for k in keep if k in ru}
+    out["kernel"] = out.get("kernel", "").split(" ")[0]
+    if "update" in ru:
+        out["update_frac"] = _r(ru["update"]["frac"])
+    return out
+
+
+def compact_line(full, detail_file=None):
+    """the <= 4 KB stdout line: the headline keys, config, the trimmed rollout and
+    update rooflines, the CPU baseline's numbers and one summary per extra shape; everything
+    else (event rates, notes, burst timings, the one-rank RCCL timing) stays in the detail file
+    the line names"""
+    keys = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data")
+    out = {k: full[k] for k in keys if k in full}
+    cfg = dict(full.get("config", {}))
+    xc = cfg.pop("exchange_check", None)
+    if xc is not None:
+        cfg["exchange_checked"] = bool(xc.get("checked")) and bool(xc.get("bitwise_equal_to_reference"))
+    out["config"] = cfg
+    for k in ("ppo_update_ms", "rollout_env_steps_per_s"):
+        if k in full:
+            out[k] = _r(full[k])
+    if "regime" in full:
+        out["regime"] = full["regime"]
+    if "roofline" in full:
+        out["roofline"] = _trim_roofline(full["roofline"])
+    if "roofline_update" in full:
+        out["roofline_update"] = _trim_update(full["roofline_update"])
+    if "cpu_baseline" in full:
+        c = full["cpu_baseline"]
+        ac = c.get("all_cores", {})
+        out["cpu_baseline"] = {
+            "value": _r(c["value"]), "unit": c["unit"], "cores": c["cores"], "kind": c["kind"],
+            "sample": c["sample"][:120],
+            "physics_only": _r(c.get("physics_only_env_steps_per_s")),
+            "train_ms": _r(c.get("train_ms_per_1001_step_episode")),
+            "all_cores": {"threads": ac.get("threads"), "env_steps_per_s": _r(ac.get("env_steps_per_s")),
+                          "cpu": ac.get("cpu_model")}}
+    if "configs" in full:
+        sm = {}
+        for name, c in full["configs"].items():
+            s = {"env_steps_per_s": _r(c.get("env_steps_per_s"))}
+            if "rollout_ms" in c:
+                s["rollout_ms"] = _r(c["rollout_ms"])
+            if "physics_ms_per_launch" in c:
+                s["physics_ms"] = _r(c["physics_ms_per_launch"])
+            if "ppo_update_ms" in c:
+                s["ppo_update_ms"] = _r(c["ppo_update_ms"])
+            if "roofline" in c:
+                s["frac"] = _r(c["roofline"]["frac"], 3)
+            if "roofline_update" in c:
+                s["update_frac"] = _r(c["roofline_update"]["frac"], 3)
+            sm[name] = s
+        out["configs"] = sm
+    if "rehearsal" in full:
+        out["rehearsal"] = full["rehearsal"]
+    if detail_file:
+        out["detail_file"] = detail_file
+    line = json.dumps(out, separators=(",", ":"))
+    if len(line) >= LINE_LIMIT:  # never lose the headline: drop the optional parts first
+        for k in ("configs", "regime", "rollout_env_steps_per_s"):
+            out.pop(k, None)
+            line = json.dumps(out, separators=(",", ":"))
+            if len(line) < LINE_LIMIT:
+                break
+    return line
+
+
+def write_detail(full, path):
+    """the full result (every roofline field, event rates, notes) as indented JSON; returns the
+    repo-relative path named in the line, or None if it cannot be written"""
+    try:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1)
+    except OSError as ex:
+        print(f"bench: detail file not written ({ex})", file=sys.stderr)
+        return None
+    return os.path.relpath(path, ROOT)
+
+
 def _claim_stdout():
     """the driver reads stdout for ONE JSON line; libraries print to fd 1 on their own (RCCL's
     version banner at the first collective), so fd 1 goes to stderr for the whole run and the
@@ -433,7 +542,7 @@ def allreduce_one_rank(wk, eng, args, horizon, update_index):
             "note": "one-rank RCCL communicator on this GPU: the collective path of every rank"}
 
 
-def ipc_exchange_setup(wk, eng, mk_engine, rank, world, horizon, dist, torch, np):
+def ipc_exchange_setup(wk, eng, mk_engine, rank, world, horizon, dist, torch, np, rehearse=False):
     """N > 1 with --exchange ipc: map the peers' exchange regions (every rank joins
     the record all-gather, also when its own handle failed), run one test round on exact small
     integers, vote; then check the one-shot exchange against an EXACT reference over several
@@ -455,11 +564,16 @@ def ipc_exchange_setup(wk, eng, mk_engine, rank, world, horizon, dist, torch, np
 
     check = {"test_round": False, "checked": False}
     ok = True
+    # rehearsal-only fault injection: this rank reports a wrong test-round sum,
+    # so every rank must take the fallback exchange and still print exactly one line
+    fault_rank = int(os.environ.get("WK_BENCH_FAULT_RANK", "-1")) if rehearse else -1
     try:
         eng.comm_init_ipc(rank, world, allgather)
         check["region"] = "uncached device memory" if eng.comm_info()[1] else "hipMalloc"
         base = (np.arange(wk.NPARAM) % 97).astype(np.float32)
         got = eng.allreduce_test(base + np.float32(rank + 1))
+        if rank == fault_rank:
+            got = got + np.float32(1)
         want = base * np.float32(world) + np.float32(world * (world + 1) // 2)
         ok = bool(np.array_equal(got, want))
         if not ok:
@@ -481,10 +595,11 @@ def ipc_exchange_setup(wk, eng, mk_engine, rank, world, horizon, dist, torch, np
         buf[:] = acc
 
     ref = mk_engine()
+    updates, epochs = 2, 2
+    same, t, wbytes = False, 0, b""
     try:
         ref.comm_init_host(rank, world, rank_order_sum)
         eng.snapshot()
-        updates, epochs = 2, 2
         for u in range(updates):
             for e in (eng, ref):
                 e.rollout(horizon)
@@ -493,14 +608,17 @@ def ipc_exchange_setup(wk, eng, mk_engine, rank, world, horizon, dist, torch, np
         same = (np.array_equal(w, ref.get_weights()) and np.array_equal(m, ref.get_adam()[0])
                 and np.array_equal(v, ref.get_adam()[1]) and t == ref.get_adam()[2]
                 and np.array_equal(eng.get_state(), ref.get_state()))
-        replicas = allgather(w.tobytes())
-        identical = all(r == replicas[0] for r in replicas)
+        wbytes = w.tobytes()
         eng.restore()
     except wk.WkError as ex:
         print(f"rank {rank}: IPC exchange check failed ({ex})", file=sys.stderr)
-        same, identical, t = False, False, 0
+        same, t, wbytes = False, 0, b""
     finally:
         ref.close()
+    # every rank joins the replica all-gather, also after a failure: a rank that
+    # skipped it would pair its peers' all_gather_object with main's vote and hang the job
+    replicas = allgather(wbytes)
+    identical = bool(wbytes) and all(r == replicas[0] for r in replicas)
     check.update({"checked": True, "updates": updates, "epochs_per_update": epochs,
                   "adam_steps": int(t), "bitwise_equal_to_reference": bool(same),
                   "replicas_identical": bool(identical),
@@ -555,7 +673,8 @@ def main():
     exchange = args.exchange if world > 1 else "none"
     xch_check = None
     if world > 1 and args.exchange == "ipc":
-        ok, xch_check = ipc_exchange_setup(wk, eng, mk_engine, rank, world, T, dist, torch, np)
+        ok, xch_check = ipc_exchange_setup(wk, eng, mk_engine, rank, world, T, dist, torch, np,
+                                           rehearse=args.rehearse)
         okt = torch.tensor([ok])
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)  # every rank takes the same exchange
         if not okt.item():
@@ -687,7 +806,8 @@ def main():
         out["rehearsal"] = (f"all ranks on one GPU, exchange {exchange}: a check of the "
                             "multi-rank path, not a performance number")
     if rank == 0:
-        print(json.dumps(out), file=json_out, flush=True)
+        detail = write_detail(out, args.detail_file) if args.detail_file else None
+        print(compact_line(out, detail), file=json_out, flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()

@@ -389,18 +389,25 @@ int wk_comm_init_host(wk_ctx* ctx, int rank, int nranks, wk_host_allreduce_fn fn
  * handle, then the PCI bus id of the rank's GPU); the caller all-gathers the records (any
  * control plane) and passes all of them, in rank order, to wk_comm_init_ipc, which maps the
  * peers' regions (WK_ERR_ARG if more than 4 ranks share one GPU: they would stall).  Per
- * minibatch one kernel publishes this rank's ordered block sum, waits (bounded: 2 s of the
- * GPU's constant clock) for every peer's, sums the ranks' slabs in rank order and applies
- * Adam -- no collective library, no host round trip.  A peer that never publishes fails
- * wk_ppo_update / wk_train_batch / wk_minibatch_gradient / wk_allreduce_test with WK_ERR_COMM
- * (fatal for the job, as a failed all-reduce): from the timed-out minibatch on no Adam step is
- * applied (W, m, v keep the last good minibatch's values) and no later exchange publishes, so
- * the peers time out too.  wk_minibatch_gradient and wk_train_batch(apply_adam = 0) run the
- * exchange as well (collective calls: every rank must make them), returning the sum over the
- * ranks as on an RCCL context. */
+ * minibatch one kernel publishes this rank's ordered block sum, waits (bounded: 30 s of the
+ * GPU's constant clock by default; WK_XCH_TIMEOUT_S in the environment at wk_comm_init_ipc, or
+ * wk_comm_set_timeout, changes it -- the ranks must stay within it of each other: a rank busy
+ * elsewhere longer than that while its peers have an update queued kills the job) for every
+ * peer's, sums the ranks' slabs in rank order and applies Adam -- no collective library, no host
+ * round trip.  A peer that never publishes (or gave up first) fails wk_ppo_update /
+ * wk_train_batch / wk_minibatch_gradient / wk_allreduce_test with WK_ERR_COMM, fatal for the
+ * job as a failed all-reduce: from the failed minibatch on this rank applies no Adam step and
+ * marks its flags aborted, so a late peer fails that same minibatch instead of applying it, and
+ * wk_get_adam reports the steps actually applied.  The replicas may still differ after a
+ * failure (a peer that read this rank's flag just before the abort, or blocks straddling the
+ * bound): stop the job or reload a checkpoint on every rank.  wk_minibatch_gradient and
+ * wk_train_batch(apply_adam = 0) run the exchange as well (collective calls: every rank must
+ * make them), returning the sum over the ranks as on an RCCL context. */
 enum { WK_IPC_HANDLE_BYTES = 128 };
 int wk_comm_ipc_handle(wk_ctx* ctx, uint8_t* handle /* WK_IPC_HANDLE_BYTES */);
 int wk_comm_init_ipc(wk_ctx* ctx, int rank, int nranks, const uint8_t* handles /* nranks * 128 */);
+/* the IPC exchange's bounded peer wait, in seconds (0 < seconds <= 1e6) */
+int wk_comm_set_timeout(wk_ctx* ctx, double seconds);
 /* the context's minibatch exchange: *kind 0 none, 1 RCCL, 2 host callback, 3 IPC; *flags bit 0:
  * the IPC exchange region is uncached device memory (else coarse-grained hipMalloc memory) */
 int wk_comm_info(wk_ctx* ctx, int* kind, int* flags);
@@ -445,9 +452,12 @@ int wk_time_gradient(wk_ctx* ctx, int minibatch, int reps, double* ms_per_launch
 int wk_time_gradient_ex(wk_ctx* ctx, int minibatch, int reps, int flags, double* ms_per_launch);
 
 /* The rollout kernel's mapping as launched: lanes per walker (1, 2, 4 or 16), walkers per
- * wave (fewer than 64 / lanes for the sparse quad mapping) and the wave count of one rollout
- * launch -- bench.py's VALU ceiling (one wave per SIMD below 1,024 waves). */
-int wk_rollout_mapping(wk_ctx* ctx, int* lanes_per_walker, int* walkers_per_wave, int64_t* waves);
+ * wave (fewer than 64 / lanes for the sparse quad mapping), the waves that hold walkers and
+ * (waves_launched, nullable) the waves the grid launches -- the split kernels launch whole
+ * 4-wave blocks whose idle waves replay the last walker.  bench.py's VALU ceiling is priced on
+ * the launched grid (one wave per SIMD below 1,024 waves). */
+int wk_rollout_mapping(wk_ctx* ctx, int* lanes_per_walker, int* walkers_per_wave, int64_t* waves,
+                       int64_t* waves_launched);
 
 /* Which matrix-core gradient kernel the update launches for a per-GPU minibatch of `minibatch`
  * samples (0 = config Minibatch): 0 producer / consumer waves (k_ppo_grad_ws), 1 tile-parallel

@@ -208,6 +208,7 @@ public static class Wk
     [DllImport(Lib)] public static extern int wk_comm_ipc_handle(IntPtr ctx, byte[] handle);
     [DllImport(Lib)] public static extern int wk_comm_init_ipc(IntPtr ctx, int rank, int nRanks, byte[] handles);
     [DllImport(Lib)] public static extern int wk_comm_info(IntPtr ctx, out int kind, out int flags);
+    [DllImport(Lib)] public static extern int wk_comm_set_timeout(IntPtr ctx, double seconds);
     [UnmanagedFunctionPointer(CallingConvention.Cdecl)] public delegate int HostAllReduce(IntPtr buf, int n, IntPtr user);
     [DllImport(Lib)] public static extern int wk_comm_init_host(IntPtr ctx, int rank, int nRanks, HostAllReduce fn, IntPtr user);
 
@@ -238,7 +239,7 @@ public static class Wk
     [DllImport(Lib)] public static extern int wk_snapshot(IntPtr ctx, int op);
     [DllImport(Lib)] public static extern int wk_time_gradient(IntPtr ctx, int minibatch, int reps, out double msPerLaunch);
     [DllImport(Lib)] public static extern int wk_time_gradient_ex(IntPtr ctx, int minibatch, int reps, int flags, out double msPerLaunch);
-    [DllImport(Lib)] public static extern int wk_rollout_mapping(IntPtr ctx, out int lanesPerWalker, out int walkersPerWave, out long waves);
+    [DllImport(Lib)] public static extern int wk_rollout_mapping(IntPtr ctx, out int lanesPerWalker, out int walkersPerWave, out long waves, out long wavesLaunched);
     [DllImport(Lib)] public static extern int wk_grad_kernel(IntPtr ctx, int minibatch);
 
     public static string LastError(IntPtr ctx) => Marshal.PtrToStringAnsi(wk_last_error(ctx)) ?? "";

@@ -99,6 +99,7 @@ struct wk_ctx {
   uint64_t xch_seq = 0;
   uint32_t* xch_err = nullptr;         // device word: a peer never published
   bool xch_uncached = false;           // the region is uncached device memory (else hipMalloc)
+  uint64_t xch_timeout_ticks = 0;      // bounded peer wait (WK_XCH_TIMEOUT_S / wk_comm_set_timeout)
   // profiling
   int prof = 0;  // profile level
   struct Ev { int kind; hipEvent_t a, b; int64_t units; };
@@ -1061,6 +1062,8 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
     x.grad_out = c->grad;
     x.seq = ++c->xch_seq;
     x.err = c->xch_err;
+    x.timeout_ticks = c->xch_timeout_ticks;
+    x.t = (uint32_t)c->adam_t;
     x.a = a;
     HIPCHK(c, wk::launch_reduce_xch_adam(x, c->stream));
     return WK_OK;
@@ -1102,18 +1105,40 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   return WK_OK;
 }
 
-// IPC contexts: WK_ERR_COMM once an exchange timed out (a peer never published; from then on
-// every exchange is a no-op and the weights keep the last good minibatch's values)
+// IPC contexts: WK_ERR_COMM once an exchange timed out or met a peer's abort (from then on every
+// exchange is a no-op); the host's Adam step count rolls back to the last step block 0 applied
+// (wk_get_adam and checkpoints report the steps actually taken)
 static int xch_status(wk_ctx* c) {
   if (!c->ipc) return WK_OK;
-  uint32_t err = 0;
-  HIPCHK(c, hipMemcpyAsync(&err, c->xch_err, sizeof err, hipMemcpyDeviceToHost, c->stream));
+  uint32_t err[2] = {0, 0};
+  HIPCHK(c, hipMemcpyAsync(err, c->xch_err, sizeof err, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (err) {
-    SETERR(c, "IPC gradient exchange: a peer did not publish its minibatch slab within %.0f s "
-           "(no Adam step applied since)", (double)wk::XCH_TIMEOUT_TICKS / 1e8);
+  if (err[0]) {
+    c->adam_t = (int)err[1];
+    SETERR(c, "IPC gradient exchange: a peer did not publish its minibatch slab within %.1f s or "
+           "gave up on it (no Adam step applied since step %u; the replicas may differ: stop the "
+           "job or reload a checkpoint on every rank)",
+           (double)c->xch_timeout_ticks / wk::XCH_TICKS_PER_S, err[1]);
     return WK_ERR_COMM;
   }
+  return WK_OK;
+}
+
+// the device's record of the last applied Adam step starts from the host's count (a checkpoint
+// or wk_set_adam may have moved it since the last exchange)
+static int xch_mark_t(wk_ctx* c) {
+  if (!c->ipc) return WK_OK;
+  HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)(c->xch_err + 1), (int)c->adam_t, 1, c->stream));
+  return WK_OK;
+}
+
+static uint64_t xch_ticks_of(double seconds) {
+  return (uint64_t)(seconds * wk::XCH_TICKS_PER_S);
+}
+
+int wk_comm_set_timeout(wk_ctx* c, double seconds) {
+  if (!c || !(seconds > 0.0) || seconds > 1.0e6) return WK_ERR_ARG;
+  c->xch_timeout_ticks = xch_ticks_of(seconds);
   return WK_OK;
 }
 
@@ -1138,22 +1163,32 @@ int wk_grad_kernel(wk_ctx* c, int minibatch) {
   return wk::grad_impl_for(c->grad_impl, minibatch > 0 ? minibatch : c->cfg.Minibatch);
 }
 
-int wk_rollout_mapping(wk_ctx* c, int* lanes_per_walker, int* walkers_per_wave, int64_t* waves) {
+int wk_rollout_mapping(wk_ctx* c, int* lanes_per_walker, int* walkers_per_wave, int64_t* waves,
+                       int64_t* waves_launched) {
   if (!c || !lanes_per_walker || !walkers_per_wave || !waves) return WK_ERR_ARG;
   const int64_t n = c->n;
-  if (c->scene.n_props > 0) {  // the one-lane scene kernel
+  int64_t launched;
+  if (c->scene.n_props > 0) {  // the one-lane scene kernel (64-thread blocks)
     *lanes_per_walker = 1; *walkers_per_wave = 64; *waves = (n + 63) / 64;
-    return WK_OK;
-  }
-  const int L = c->P.lanes;
-  *lanes_per_walker = L;
-  if (L == 4) {  // sparse quad: wpw walkers in the first 4 wpw lanes of each wave
-    *walkers_per_wave = c->P.wpw;
-    *waves = (n + c->P.wpw - 1) / c->P.wpw;
+    launched = *waves;
   } else {
-    *walkers_per_wave = 64 / L;
-    *waves = (n * L + 63) / 64;
+    const int L = c->P.lanes;
+    *lanes_per_walker = L;
+    if (L == 4) {  // sparse quad: wpw walkers in the first 4 wpw lanes of each wave
+      *walkers_per_wave = c->P.wpw;
+      *waves = (n + c->P.wpw - 1) / c->P.wpw;
+    } else {
+      *walkers_per_wave = 64 / L;
+      *waves = (n * L + 63) / 64;
+    }
+    launched = *waves;
+    if (L == 2 || L == 4) {  // k_env_side launches whole SIDE_BLOCK blocks: the idle
+      // waves of the last block still run the loop, replaying the last walker
+      constexpr int64_t wpb = wk::SIDE_BLOCK_THREADS / 64;
+      launched = (*waves + wpb - 1) / wpb * wpb;
+    }
   }
+  if (waves_launched) *waves_launched = launched;
   return WK_OK;
 }
 
@@ -1248,6 +1283,7 @@ static int ppo_update_impl(wk_ctx* c, const wk_ppo_args* args) {
     int r = returns_impl(c);
     if (r) return r;
   }
+  if (int r = xch_mark_t(c)) return r;
   const int epochs = (args && args->epochs > 0) ? args->epochs : c->cfg.Epochs;
   const int M = (args && args->minibatch > 0) ? args->minibatch : c->cfg.Minibatch;
   int Mg = (args && args->minibatch_global > 0) ? args->minibatch_global : c->cfg.MinibatchGlobal;
@@ -1302,7 +1338,9 @@ static int batch_impl(wk_ctx* c, int wpb, int B, float b_div, const float* s, co
   g.samples = B;
   g.spw = B;  // wpb 1: one wave, samples in order (the reference's sequential sums)
   g.b_div = b_div;
-  int r = minibatch(c, g, wpb, apply_adam);
+  int r = xch_mark_t(c);
+  if (r) return r;
+  r = minibatch(c, g, wpb, apply_adam);
   if (r) return r;
   std::vector<float> slab(wk::SLAB);
   HIPCHK(c, hipMemcpyAsync(slab.data(), c->grad, sizeof(float) * slab.size(), hipMemcpyDeviceToHost, c->stream));
@@ -1390,8 +1428,8 @@ int wk_comm_ipc_handle(wk_ctx* c, uint8_t* handle) {
       c->xch_uncached = true;
     }
     HIPCHK(c, hipMemset(c->xch, 0, bytes));
-    HIPCHK(c, hipMalloc((void**)&c->xch_err, sizeof(uint32_t)));
-    HIPCHK(c, hipMemset(c->xch_err, 0, sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc((void**)&c->xch_err, 2 * sizeof(uint32_t)));
+    HIPCHK(c, hipMemset(c->xch_err, 0, 2 * sizeof(uint32_t)));
   }
   hipIpcMemHandle_t h;
   HIPCHK(c, hipIpcGetMemHandle(&h, c->xch));
@@ -1443,6 +1481,14 @@ int wk_comm_init_ipc(wk_ctx* c, int rank, int nranks, const uint8_t* handles) {
   x.rank = rank;
   x.nranks = nranks;
   c->xa = x;
+  if (c->xch_timeout_ticks == 0) {  // wk_comm_set_timeout before the mapping wins
+    double sec = wk::XCH_TIMEOUT_S_DEFAULT;
+    if (const char* e = getenv("WK_XCH_TIMEOUT_S")) {
+      const double v = atof(e);
+      if (v > 0.0 && v <= 1.0e6) sec = v;
+    }
+    c->xch_timeout_ticks = xch_ticks_of(sec);
+  }
   c->xch_peers = opened;
   c->ipc = true;
   c->rank = rank;
@@ -1473,6 +1519,7 @@ int wk_allreduce_test(wk_ctx* c, float* host_buf, int n) {
     x.grad_out = out;
     x.seq = ++c->xch_seq;
     x.err = c->xch_err;
+    x.timeout_ticks = c->xch_timeout_ticks;
     x.a = wk::AdamArgs{};
     HIPCHK(c, wk::launch_reduce_xch_adam(x, c->stream));
     HIPCHK(c, hipMemcpyAsync(host_buf, out, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));

@@ -142,12 +142,23 @@ hipError_t launch_adam(const AdamArgs& a, hipStream_t s);
 // reduction and Adam (wk_comm_init_ipc): rank r's exchange region is [2][SLAB] floats
 // (double-buffered by minibatch parity) then XCH_FLAGS uint64 sequence flags, one per block of
 // the fused kernel (each block owns a span of parameter quads).
-// XCH_TIMEOUT_TICKS: the bounded wait for a peer's flag, in s_memrealtime ticks (the 100 MHz
-// constant clock): 2 s.  XCH_MAX_RANKS_PER_DEVICE: more ranks sharing one GPU stall (their
+// XCH_TIMEOUT_S_DEFAULT: the bounded wait for a peer's flag (s_memrealtime ticks of the 100 MHz
+// constant clock, XCH_TICKS_PER_S); a context takes WK_XCH_TIMEOUT_S from the environment at
+// wk_comm_init_ipc or wk_comm_set_timeout.  XCH_ABORT: the flag value of a rank whose exchange
+// timed out (or that saw an earlier timeout): a peer that reads it fails the same minibatch
+// instead of applying it.  XCH_MAX_RANKS_PER_DEVICE: more ranks sharing one GPU stall (their
 // waiting exchange blocks hold the CUs a peer's gradient kernel needs), so wk_comm_init_ipc
 // refuses them.
+// threads per block of the split (pair / quad) rollout kernels; wk_rollout_mapping reports the
+// launched grid from it
+#ifndef WK_SIDE_BLOCK
+#define WK_SIDE_BLOCK 256
+#endif
+constexpr int SIDE_BLOCK_THREADS = WK_SIDE_BLOCK;
 enum : int { XCH_FLAGS = 128, XCH_MAX_RANKS = 8, XCH_MAX_RANKS_PER_DEVICE = 4 };
-constexpr uint64_t XCH_TIMEOUT_TICKS = 200000000ull;
+constexpr double XCH_TIMEOUT_S_DEFAULT = 30.0;
+constexpr double XCH_TICKS_PER_S = 1.0e8;
+constexpr uint64_t XCH_ABORT = ~0ull;
 struct XchArgs {
   const float* partial;                // this rank's gradient-kernel block slabs [nblocks][SLAB]
   int nblocks;
@@ -156,8 +167,11 @@ struct XchArgs {
   uint64_t* flag[XCH_MAX_RANKS];       // every rank's XCH_BLOCKS flags
   int rank, nranks;
   uint64_t seq;                        // this minibatch's sequence number (from 1)
-  uint32_t* err;                       // set to 1 if a peer never published (bounded wait); once
-                                       // set, every later exchange is a no-op (no Adam)
+  uint32_t* err;                       // [0] set to 1 if a peer never published (bounded wait) or
+                                       // aborted; once set, every later exchange is a no-op (no
+                                       // Adam); [1] the Adam step t block 0 last applied
+  uint64_t timeout_ticks;              // the bounded wait (s_memrealtime ticks)
+  uint32_t t;                          // this minibatch's Adam step (with a.W)
   AdamArgs a;                          // a.W == null: exchange only (gradient-only calls)
 };
 size_t xch_region_bytes();

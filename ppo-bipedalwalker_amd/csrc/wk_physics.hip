@@ -1194,10 +1194,7 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool wri
 #ifndef WK_QUAD_WAVES
 #define WK_QUAD_WAVES 1  // waves per SIMD the quad mapping is built for
 #endif
-#ifndef WK_SIDE_BLOCK
-#define WK_SIDE_BLOCK 256
-#endif
-constexpr int SIDE_BLOCK = WK_SIDE_BLOCK;  // 4 waves: the policy's weight image is staged once per block
+constexpr int SIDE_BLOCK = SIDE_BLOCK_THREADS;  // 4 waves: the policy's weight image is staged once per block
 // Q = 1: a lane pair per walker (L = 2); Q = 2: a lane quad (L = 4, side = lane bit 0, half =
 // lane bit 1), for shards of at most one wave per SIMD, where the split shortens each wave's
 // dependent chain -- with room for every register (one wave per SIMD: no spills)

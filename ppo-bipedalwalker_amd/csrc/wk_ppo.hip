@@ -498,12 +498,17 @@ hipError_t launch_grad_reduce_adam(const float* partial, int nblocks, float* par
 // applies Adam.  A buffer is reused two minibatches later only: a rank publishes seq + 2 after
 // its exchange of seq + 1 saw every peer's seq + 1 flag, which a peer sets only once its own
 // exchange of seq -- the last read of the seq buffers -- has completed (stream order).
-// Failure: the wait is bounded by XCH_TIMEOUT_TICKS of the constant 100 MHz clock (2 s); a block
-// whose wait times out sets *err and returns without writing grad_out or applying Adam, and
-// every later exchange sees *err at entry and returns before publishing (so the peers time out
-// too and the error reaches every rank) -- W / m / v keep their values from the last good
-// minibatch.  (Only a peer that dies half-way through publishing one minibatch's flags can
-// leave that minibatch applied in some blocks and not in others; the job is dead then.)
+// Failure: the wait is bounded by x.timeout_ticks of the constant 100 MHz clock (30 s unless
+// WK_XCH_TIMEOUT_S / wk_comm_set_timeout say otherwise; ranks must stay within it of each other).
+// A block whose wait times out, or that finds a peer's flag at XCH_ABORT, sets err[0], overwrites
+// its own flag with XCH_ABORT and returns without writing grad_out or applying Adam; every later
+// exchange sees err[0] at entry, writes XCH_ABORT into its flag and returns, so a late peer fails
+// at once on that minibatch (it reads the abort value instead of this rank's sequence number)
+// rather than applying it.  Block 0 records the last Adam step it applied in err[1], so the host
+// rolls its step count back.  Not a consensus protocol: a peer that read this rank's sequence
+// number before the abort overwrote it (a wait that ended within the same few microseconds), or
+// blocks of one rank that straddle the timeout, leave the replicas' W / m / v differing -- after
+// WK_ERR_COMM the job must stop or reload a checkpoint on every rank.
 __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
   __shared__ float4 gs[RG][QB];
   __shared__ int live;  // no exchange has timed out (entry), and this block's wait completed
@@ -533,7 +538,12 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
   }
   gs[gi][qi] = acc;
   __syncthreads();
-  if (!live) return;  // an earlier exchange timed out (block-uniform: read after the barrier)
+  const int t = threadIdx.x;
+  if (!live) {  // an earlier exchange failed (block-uniform: read after the barrier)
+    if (t == 0)
+      __hip_atomic_store(x.flag[x.rank] + blockIdx.x, XCH_ABORT, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   const int buf = (int)(x.seq & 1u);
   float mine = 0.0f;
   if (gi < 4 && q < SLAB / 4) {  // stage 2: this rank's ordered sum, published
@@ -552,23 +562,27 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
   // visibility: the workgroup barrier alone does not wait for other waves' stores)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const int t = threadIdx.x;
   if (t == 0)
     __hip_atomic_store(x.flag[x.rank] + blockIdx.x, x.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   if (t < x.nranks && t != x.rank) {
     const uint64_t* f = x.flag[t] + blockIdx.x;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < x.seq) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > XCH_TIMEOUT_TICKS) {
-        atomicOr(x.err, 1u);  // a peer is gone: report, never hang the GPU
-        live = 0;
-        break;
-      }
+    uint64_t seen;
+    while ((seen = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) < x.seq) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > x.timeout_ticks) break;
       __builtin_amdgcn_s_sleep(2);
+    }
+    if (seen < x.seq || seen == XCH_ABORT) {  // a peer is gone or gave up: report, never hang
+      atomicOr(x.err, 1u);
+      live = 0;
     }
   }
   __syncthreads();
-  if (!live) return;  // no grad_out, no Adam: the weights keep the last good minibatch's values
+  if (!live) {  // no grad_out, no Adam; a late peer reading this flag fails this minibatch too
+    if (t == 0)
+      __hip_atomic_store(x.flag[x.rank] + blockIdx.x, XCH_ABORT, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale peer lines
   if (gi < 4 && q < SLAB / 4) {
     float sum = x.rank == 0 ? mine : x.slab[0][(size_t)buf * SLAB + p];
@@ -577,6 +591,8 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
     x.grad_out[p] = sum;
     if (adam_lane) adam_apply(x.a, p, sum, m0, v0, w0);
   }
+  if (blockIdx.x == 0 && t == 0 && x.a.W != nullptr)
+    __hip_atomic_store(x.err + 1, x.t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 size_t xch_region_bytes() { return sizeof(float) * 2 * SLAB + sizeof(uint64_t) * XCH_FLAGS; }
 hipError_t launch_reduce_xch_adam(const XchArgs& x, hipStream_t s) {

@@ -42,7 +42,7 @@ EXPORTS = [
     "wk_comm_unique_id", "wk_comm_init", "wk_comm_init_host", "wk_allreduce_test", "wk_profile_enable",
     "wk_profile_get", "wk_profile_reset", "wk_count_events", "wk_snapshot", "wk_time_gradient",
     "wk_time_gradient_ex", "wk_grad_kernel", "wk_rollout_mapping",
-    "wk_comm_ipc_handle", "wk_comm_init_ipc", "wk_comm_info",
+    "wk_comm_ipc_handle", "wk_comm_init_ipc", "wk_comm_info", "wk_comm_set_timeout",
 ]
 
 
@@ -237,11 +237,13 @@ def load_library(path=None):
         "wk_comm_init_host": (I, [P, I, I, HOST_ALLREDUCE_FN, P]),
         "wk_time_gradient": (I, [P, I, I, C.POINTER(C.c_double)]),
         "wk_time_gradient_ex": (I, [P, I, I, I, C.POINTER(C.c_double)]),
-        "wk_rollout_mapping": (I, [P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int64)]),
+        "wk_rollout_mapping": (I, [P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int64),
+                                   C.POINTER(C.c_int64)]),
         "wk_comm_info": (I, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "wk_grad_kernel": (I, [P, I]),
         "wk_comm_ipc_handle": (I, [P, P]),
         "wk_comm_init_ipc": (I, [P, I, I, P]),
+        "wk_comm_set_timeout": (I, [P, C.c_double]),
         "wk_profile_enable": (I, [P, I]),
         "wk_profile_get": (I, [P, C.POINTER(Profile)]),
         "wk_profile_reset": (I, [P]),
@@ -711,6 +713,11 @@ class Engine:
             raise WkError(f"wk_comm_init_ipc: rank(s) {bad} have no exchange record")
         self.comm_init_ipc_records(rank, nranks, records)
 
+    def comm_set_timeout(self, seconds):
+        """wk_comm_set_timeout: the IPC exchange's bounded peer wait (default 30 s, or
+        WK_XCH_TIMEOUT_S at the mapping)"""
+        self._chk(self.lib.wk_comm_set_timeout(self.h, float(seconds)), "wk_comm_set_timeout")
+
     COMM_KINDS = {0: "none", 1: "rccl", 2: "host", 3: "ipc"}
 
     def comm_info(self):
@@ -745,12 +752,14 @@ class Engine:
         return ms.value
 
     def rollout_mapping(self):
-        """wk_rollout_mapping: {lanes_per_walker, walkers_per_wave, waves} of a rollout launch"""
+        """wk_rollout_mapping: {lanes_per_walker, walkers_per_wave, waves (holding walkers),
+        waves_launched (the grid, whole 4-wave blocks for the split kernels)} of a rollout launch"""
         L, w = C.c_int(), C.c_int()
-        n = C.c_int64()
-        self._chk(self.lib.wk_rollout_mapping(self.h, C.byref(L), C.byref(w), C.byref(n)),
-                  "wk_rollout_mapping")
-        return {"lanes_per_walker": L.value, "walkers_per_wave": w.value, "waves": n.value}
+        n, nl = C.c_int64(), C.c_int64()
+        self._chk(self.lib.wk_rollout_mapping(self.h, C.byref(L), C.byref(w), C.byref(n),
+                                              C.byref(nl)), "wk_rollout_mapping")
+        return {"lanes_per_walker": L.value, "walkers_per_wave": w.value, "waves": n.value,
+                "waves_launched": nl.value}
 
     # -- counting replay / snapshots --
     def count_events(self, k):

@@ -1,0 +1,78 @@
+"""CPU: bench.py's stdout line stays parseable by the driver (round 4's 20 KB line
+was lost).  The compact line is built from a full result -- round 4's real 20,216-byte line
+(`profiles/r04_bench.json`, every configs sub-line with its rooflines) -- and must be one JSON line
+under 4 KB that keeps the headline keys, the trimmed rollout / update rooflines, the CPU
+baseline and a summary of every extra shape."""
+import copy
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402  (module level imports nothing heavy)
+
+HEAD = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config")
+
+
+def _full():
+    with open(os.path.join(ROOT, "profiles", "r04_bench.json")) as f:
+        return json.load(f)
+
+
+def test_compact_line_under_4kb_keeps_the_contract():
+    full = _full()
+    assert len(json.dumps(full)) > 4096  # the case that broke the driver record
+    line = bench.compact_line(full, "gpurun_out/bench_detail.json")
+    assert "\n" not in line and len(line) < 4096, len(line)
+    out = json.loads(line)
+    for k in HEAD:
+        assert k in out, k
+    assert out["value"] == full["value"] and out["ms_per_step"] == full["ms_per_step"]
+    rf = out["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "peak_no_fma", "frac_no_fma",
+              "flop_per_env_step_counted", "mean_launch_ms", "kernel"):
+        assert k in rf, k
+    assert abs(rf["frac"] - full["roofline"]["frac"]) < 1e-3 * full["roofline"]["frac"]
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3 * rf["frac"]
+    ru = out["roofline_update"]
+    assert ru["kernel"] == "k_ppo_grad_ws" and "mean_launch_us" in ru and "update_frac" in ru
+    cb = out["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample", "physics_only", "train_ms", "all_cores"):
+        assert k in cb, k
+    assert cb["all_cores"]["threads"] == 16
+    assert set(out["configs"]) == set(full["configs"])
+    for name, c in out["configs"].items():
+        assert "env_steps_per_s" in c and "frac" in c, name
+    assert out["detail_file"] == "gpurun_out/bench_detail.json"
+
+
+def test_compact_line_drops_optional_parts_before_the_headline():
+    full = _full()
+    for i in range(40):  # a pathological number of extra shapes
+        full["configs"][f"extra_{i}"] = copy.deepcopy(full["configs"]["config3_full_4096"])
+    line = bench.compact_line(full)
+    assert len(line) < 4096
+    out = json.loads(line)
+    assert "configs" not in out and out["value"] == full["value"] and "roofline" in out
+
+
+def test_multirank_line_carries_the_exchange_check():
+    full = _full()
+    for k in ("configs", "cpu_baseline"):
+        full.pop(k)
+    full["n_gpus"] = 8
+    full["config"]["exchange"] = "ipc"
+    full["config"]["exchange_check"] = {"checked": True, "bitwise_equal_to_reference": True,
+                                        "replicas_identical": True, "test_round": True}
+    out = json.loads(bench.compact_line(full))
+    assert out["config"]["exchange"] == "ipc" and out["config"]["exchange_checked"] is True
+
+
+def test_detail_file_round_trip(tmp_path):
+    full = _full()
+    p = tmp_path / "sub" / "detail.json"
+    rel = bench.write_detail(full, str(p))
+    assert rel is not None and json.load(open(p)) == full

@@ -48,7 +48,7 @@ def c_kind(p):
     t = p.split()[0:-1]
     t = " ".join(t)
     return {"int": "i32", "int32_t": "i32", "uint32_t": "u32", "uint64_t": "u64", "int64_t": "i64",
-            "float": "f32", "size_t": "usize"}[t]
+            "float": "f32", "double": "f64", "size_t": "usize"}[t]
 
 
 def cs_kind(p):
@@ -59,7 +59,7 @@ def cs_kind(p):
     t = toks[0]
     if t.endswith("[]") or t.endswith("[]?") or t in ("IntPtr", "string", "HostAllReduce"):
         return "ptr"
-    return {"int": "i32", "uint": "u32", "ulong": "u64", "long": "i64", "float": "f32",
+    return {"int": "i32", "uint": "u32", "ulong": "u64", "long": "i64", "float": "f32", "double": "f64",
             "UIntPtr": "usize"}[t]
 
 

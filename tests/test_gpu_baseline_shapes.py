@@ -202,7 +202,7 @@ def test_headline_65536_rollout_T64_bitexact(wk, orc, materials):
     n = 65536
     eng, ag, tr = _rollout_and_replay(wk, orc, n, T_H, materials, Minibatch=n, Epochs=1)
     assert eng.rollout_mapping() == {"lanes_per_walker": 2, "walkers_per_wave": 32,
-                                     "waves": n * 2 // 64}
+                                     "waves": n * 2 // 64, "waves_launched": n * 2 // 64}
     _check_policy_outputs(orc, ag, tr, n, T_H)
     eng.close()
 

@@ -44,3 +44,27 @@ def test_bench_two_rank_rehearsal(exchange):
     assert "quad" in out["roofline"]["kernel"]
     assert out["value"] > 0 and out["ms_per_step"] > 0
     assert abs(out["value"] - 4096 * 8 * 2 / (out["ms_per_step"] * 2e-3)) < 1e-6 * out["value"]
+
+
+def test_bench_ipc_fallback_when_one_rank_fails():
+    """rank 1's IPC test round reports a wrong sum (WK_BENCH_FAULT_RANK, honoured
+    only under --rehearse); every rank must vote the IPC exchange down, rebuild its engine, take
+    the fallback (the host all-reduce over gloo in a rehearsal, RCCL on a real node) and the job
+    must still end with rc 0 and exactly one JSON line"""
+    cmd = ["timeout", "-k", "10", "240", sys.executable, "-m", "torch.distributed.run",
+           "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--rehearse", "--walkers-global", "4096",
+           "--horizon", "8", "--epochs", "1", "--regime-iters", "1", "--exchange", "ipc",
+           "--detail-file", ""]
+    env = dict(os.environ, WK_BENCH_FAULT_RANK="1")
+    p = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       env=env)
+    assert p.returncode == 0, p.stdout[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["config"]["exchange"] == "host (gloo)"
+    assert out["config"]["exchange_checked"] is False
+    assert "rank 1: IPC exchange test gave wrong sums" in p.stdout
+    assert out["value"] > 0 and len(lines[0]) < 4096

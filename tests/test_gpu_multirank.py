@@ -50,12 +50,12 @@ def _adam_t1(w, g, alpha=np.float32(0.001), beta1=0.9, beta2=0.999, eps=np.float
     return w - ((mh / den) * alpha), m, v
 
 
-def _run_two_ranks(out, mode, n=2):
+def _run_two_ranks(out, mode, n=2, **extra_env):
     port = _free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK="0",
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **extra_env)
         procs.append(subprocess.Popen(
             ["timeout", "-k", "10", "240", sys.executable,
              os.path.join(ROOT, "tests", "workers", "multirank_worker.py"), str(out), mode],
@@ -127,15 +127,32 @@ def test_three_ranks_ipc_rank_order_sum(tmp_path):
 
 def test_ipc_peer_never_publishes(tmp_path):
     """rank 1 maps the exchange and then never publishes.  Rank 0's update
-    fails with WK_ERR_COMM after the stated 2-s bound (XCH_TIMEOUT_TICKS of the 100 MHz constant
-    clock; the later minibatches return at once) and applies no Adam step: W, m and v are
-    bit-identical before and after"""
-    r0, _ = _run_two_ranks(tmp_path, "ipc_silent")
+    fails with WK_ERR_COMM after the bound (WK_XCH_TIMEOUT_S = 2 s of the 100 MHz constant clock
+    here; 30 s by default; the later minibatches return at once) and applies no Adam step: W, m
+    and v are bit-identical before and after"""
+    r0, _ = _run_two_ranks(tmp_path, "ipc_silent", WK_XCH_TIMEOUT_S="2")
     print(f"failing update took {float(r0['elapsed']):.2f} s: {r0['raised']}")
     assert "did not publish" in str(r0["raised"])
     assert 1.5 <= float(r0["elapsed"]) <= 8.0
     for k in ("w", "m", "v"):
         np.testing.assert_array_equal(r0[k + "_before"], r0[k + "_after"], err_msg=k)
+
+
+def test_ipc_late_peer_fails_the_same_minibatch(tmp_path):
+    """rank 1 is alive but late (busy past the 2-s bound while rank 0 has its update
+    queued).  Rank 0 times out and marks its flags aborted; rank 1 then fails the same minibatch
+    at once instead of applying it.  Both replicas keep the first update's W / m / v bit for bit,
+    and both report Adam step 1 (the steps applied), not 2 (the steps attempted)"""
+    r0, r1 = _run_two_ranks(tmp_path, "ipc_late", WK_XCH_TIMEOUT_S="2")
+    print(f"rank 0 failed after {float(r0['elapsed']):.2f} s, rank 1 after {float(r1['elapsed']):.2f} s")
+    for r in (r0, r1):
+        assert "did not publish" in str(r["raised"]) and "step 1" in str(r["raised"])
+        assert int(r["t1"]) == 1 and int(r["t2"]) == 1
+        for k in ("w", "m", "v"):
+            np.testing.assert_array_equal(r[k + "1"], r[k + "2"], err_msg=k)
+    np.testing.assert_array_equal(r0["w2"], r1["w2"])
+    assert 1.5 <= float(r0["elapsed"]) <= 8.0
+    assert float(r1["elapsed"]) < 1.0  # the abort value, not a second timeout
 
 
 def test_ipc_refuses_more_than_four_ranks_per_gpu(wk):

@@ -30,11 +30,14 @@ def _engine(wk, n, ordered, **cfg):
             os.environ["WK_ORDER"] = old
 
 
-@pytest.mark.parametrize("n,lanes", [(3000, 4), (4096, 4), (20011, 2), (40000, 2)])
-def test_lane_order_is_invisible(wk, n, lanes):
+@pytest.mark.parametrize("n,lanes,rough", [(3000, 4, 0), (4096, 4, 0), (20011, 2, 0), (40000, 2, 0),
+                                           (20011, 2, 1)])
+def test_lane_order_is_invisible(wk, n, lanes, rough):
+    """rough = 1: the rough-floor pair kernel fills its per-walker terrain column in
+    LDS from the reordered walker id"""
     T = 16
     cfg = dict(Horizon=T, Minibatch=n * T // 4, Epochs=1, RandomizeStart=1, RandomizeMaterial=1,
-               MaxTimesteps=30, LanesPerWalker=lanes)
+               MaxTimesteps=30, LanesPerWalker=lanes, RoughFloor=rough)
     a, b = _engine(wk, n, True, **cfg), _engine(wk, n, False, **cfg)
     # Environment.Reset of a random 40 % (wk_reset: those walkers continue post-reset, the
     # floor first in their body list), so every launch starts with both kinds of walker

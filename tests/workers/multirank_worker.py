@@ -62,6 +62,44 @@ if mode == "ipc_silent":
     eng.close()
     dist.destroy_process_group()
     sys.exit(0)
+if mode == "ipc_late":
+    # a slow but live peer.  One good update on both ranks, then rank 0 updates while
+    # rank 1 is busy past the bound; rank 0 fails and aborts its flags, and rank 1, arriving
+    # late, must fail the SAME minibatch at once (it reads the abort, not a sequence number)
+    # instead of applying it -- both replicas keep the first update's W / m / v, and both report
+    # the Adam steps actually applied (1), not the steps attempted
+    import time
+
+    def allgather(b):
+        out = [None] * world
+        dist.all_gather_object(out, b)
+        return out
+    eng.comm_init_ipc(rank, world, allgather)
+    eng.rollout(T)
+    eng.ppo_update(update_index=0)
+    eng.sync()
+    w1, (m1, v1, t1) = eng.get_weights(), eng.get_adam()
+    eng.rollout(T)
+    eng.sync()
+    dist.barrier()
+    if rank == 1:
+        dist.barrier()  # busy elsewhere until rank 0 has given up
+    t0 = time.perf_counter()
+    try:
+        eng.ppo_update(update_index=1)
+        raised = ""
+    except wk.WkError as ex:
+        raised = str(ex)
+    elapsed = time.perf_counter() - t0
+    if rank == 0:
+        dist.barrier()
+    w2, (m2, v2, t2) = eng.get_weights(), eng.get_adam()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), elapsed=elapsed, raised=raised, w1=w1, m1=m1,
+             v1=v1, t1=t1, w2=w2, m2=m2, v2=v2, t2=t2)
+    dist.barrier()
+    eng.close()
+    dist.destroy_process_group()
+    sys.exit(0)
 solo = wk.Engine(n_local, seed=SEED, **cfg)  # same shard, no communicator
 if mode == "ipc":
     def allgather(b):
