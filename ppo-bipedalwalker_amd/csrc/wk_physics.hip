@@ -41,19 +41,35 @@
 
 namespace wk {
 
-// Optional per-region wave-time profile (build with -DWK_REGION_PROF; scripts/region_prof.py):
-// s_memtime deltas accumulated per wave, summed over waves into g_region_prof.
+// Optional per-region wave-time profile (build with -DWK_REGION_PROF; scripts/region_prof.py).
+// Wave-level: every mark is executed by the lanes that run the code it ends,
+// and the wave's FIRST ACTIVE lane charges the s_memtime delta since the wave's previous mark --
+// whichever lanes executed that one -- to the region the mark names, in a per-wave LDS record.
+// So a region's time is the time the WAVE spent executing it (whatever its lane mask), and 'other'
+// is only the code between regions (slot selection, joins, the env-step tail).  Each mark also
+// adds the number of active lanes, so lanes / count is the region's mean active lanes.
+enum { RP_JOINT, RP_INTEG, RP_AABB_LL, RP_AABB_LF, RP_AABB_BF, RP_SAT_LL, RP_SAT_LF, RP_SAT_BF,
+       RP_CON_LL, RP_CON_LF, RP_CON_BF, RP_IMP_LL, RP_IMP_LF, RP_IMP_BF, RP_POLICY, RP_OTHER, RP_N };
 #ifdef WK_REGION_PROF
-static __device__ unsigned long long g_region_prof[16];  // (probe builds; read in part 1)
-struct RegionProf { uint64_t acc[8]; uint64_t t; };
+static __device__ unsigned long long g_region_prof[3 * RP_N];  // ticks, lane sums, counts
+struct WaveProf { unsigned long long acc[RP_N]; unsigned long long lanes[RP_N]; unsigned cnt[RP_N]; unsigned long long t; };
+struct RegionProf { WaveProf* w; };
 DEV void rp_mark(RegionProf* p, int r) {
-  if (p) { const uint64_t t = __builtin_amdgcn_s_memtime(); p->acc[r] += t - p->t; p->t = t; }
+  if (!p) return;
+  const uint64_t ex = __builtin_amdgcn_read_exec();
+  const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if (lane == __builtin_ffsll((long long)ex) - 1) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    p->w->acc[r] += t - p->w->t;
+    p->w->t = t;
+    p->w->lanes[r] += (unsigned long long)__builtin_popcountll(ex);
+    p->w->cnt[r] += 1u;
+  }
 }
 #else
 struct RegionProf {};
 DEV void rp_mark(RegionProf*, int) {}
 #endif
-enum { RP_JOINT, RP_INTEG, RP_AABB, RP_SAT, RP_CONTACT, RP_IMPULSE, RP_POLICY, RP_OTHER };
 
 struct EnvState {
   Poly<6> lll, llu, rll, rlu;
@@ -343,7 +359,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
     aabb(B, b0x, b0y, b1x, b1y);
     ov = mnx < b1x && mxx > b0x && mny < b1y && mxy > b0y;
   }
-  rp_mark(rp, RP_AABB);
+  rp_mark(rp, RP_AABB_LL + EVK);
   DUP(1, { const auto Ap = perturbed(A); sink(aabb_overlap(Ap, B) ? 1.0f : 0.0f); });
   if (!ov) return;
   if (ec) ec[EV_AABB_LL + EVK]++;
@@ -365,7 +381,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   else if constexpr (FLAT) hit = sat_floor<NA, NA == 6>(A, B, mnx, mny, mxx, mxy, n, depth, &axa);
   else if constexpr (KEEP) hit = sat<NA, NB, false, true>(A, B, n, depth, &axa, &axb);
   else hit = sat<NA, NB, GENERIC, true>(A, B, n, depth);
-  rp_mark(rp, RP_SAT);
+  rp_mark(rp, RP_SAT_LL + EVK);
   DUP(2, { const auto Ap = perturbed(A); V2 n2; float d2;
            const bool h2 = sat(Ap, B, n2, d2); sink(n2.x); sink(n2.y); sink(d2); sink(h2 ? 1.0f : 0.0f); });
   if (!hit) return;
@@ -376,7 +392,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   else if constexpr (KEEP && FLAT) nc = contact_points_floor<NA, FS>(A, axa, n, c0, c1, frec);
   else if constexpr (KEEP) nc = contact_points_ax<NA, NB, FS>(A, axa, B, axb, n, c0, c1, frec);
   else nc = contact_points<NA, NB, GENERIC>(A, B, n, c0, c1);
-  rp_mark(rp, RP_CONTACT);
+  rp_mark(rp, RP_CON_LL + EVK);
   DUP(3, { const auto Ap = perturbed(A); V2 e0, e1;
            const int k2 = contact_points(Ap, B, n, e0, e1); sink(e0.x); sink(e1.y); sink((float)k2); });
   if (TRACE && tr && pi >= 0) {
@@ -423,7 +439,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   if (TRACE && tr && pi >= 0) { tr->impulse[pi][0] = j; tr->impulse[pi][1] = jf; }
   apply_impulses<BSTATIC>(bA, bB, n, j, rA, rB);
   apply_impulses<BSTATIC>(bA, bB, tangent, jf, rAF, rBF);
-  rp_mark(rp, RP_IMPULSE);
+  rp_mark(rp, RP_IMP_LL + EVK);
   DUP(4, { Dyn dA2 = dA, dB2 = dB; const float z = opaque_zero();
            Body cA{A.cx + z, A.cy, &dA2, mA.im, mA.ii}; Body cB{B.cx, B.cy, &dB2, mB.im, mB.ii};
            V2 sA, sB, sAF, sBF;
@@ -1258,8 +1274,12 @@ void k_env_side(EnvParams P, StepArgs A) {
   uint32_t t = A.rng_t[e];
   uint32_t fault = 0;
 #ifdef WK_REGION_PROF
-  RegionProf rpv = {};
-  rpv.t = __builtin_amdgcn_s_memtime();
+  __shared__ WaveProf wprof[SIDE_BLOCK / 64];
+  RegionProf rpv{&wprof[threadIdx.x >> 6]};
+  if ((threadIdx.x & 63) == 0) {
+    for (int r = 0; r < RP_N; r++) { rpv.w->acc[r] = 0; rpv.w->lanes[r] = 0; rpv.w->cnt[r] = 0; }
+    rpv.w->t = __builtin_amdgcn_s_memtime();
+  }
   RegionProf* rp = &rpv;
 #else
   RegionProf* rp = nullptr;
@@ -1372,7 +1392,11 @@ void k_env_side(EnvParams P, StepArgs A) {
   if (active && half == 0) store_side(s, A.st, lane_opaque((uint32_t)e), side);
 #ifdef WK_REGION_PROF
   if ((threadIdx.x & 63) == 0)
-    for (int r = 0; r < 8; r++) atomicAdd(&g_region_prof[r], (unsigned long long)rpv.acc[r]);
+    for (int r = 0; r < RP_N; r++) {
+      atomicAdd(&g_region_prof[r], rpv.w->acc[r]);
+      atomicAdd(&g_region_prof[RP_N + r], rpv.w->lanes[r]);
+      atomicAdd(&g_region_prof[2 * RP_N + r], (unsigned long long)rpv.w->cnt[r]);
+    }
 #endif
   fault |= (uint32_t)pswap((float)fault);
   if (leader) {
@@ -1575,10 +1599,10 @@ hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipS
 }
 #endif  // WK_PART(3)
 #if defined(WK_REGION_PROF) && WK_PART(1)
-extern "C" int wk_region_prof(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_region_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+extern "C" int wk_region_prof(unsigned long long* out, int reset) {  // out[3 * RP_N]
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_region_prof), sizeof(unsigned long long) * 3 * RP_N) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[3 * RP_N] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_region_prof), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;
