@@ -54,8 +54,13 @@ enum { RP_JOINT, RP_INTEG, RP_AABB_LL, RP_AABB_LF, RP_AABB_BF, RP_SAT_LL, RP_SAT
 static __device__ unsigned long long g_region_prof[3 * RP_N];  // ticks, lane sums, counts
 struct WaveProf { unsigned long long acc[RP_N]; unsigned long long lanes[RP_N]; unsigned cnt[RP_N]; unsigned long long t; };
 struct RegionProf { WaveProf* w; };
-DEV void rp_mark(RegionProf* p, int r) {
+// deps: values the region computes -- the empty asm makes them ready before the stamp, so the
+// scheduler cannot sink the region's arithmetic past its mark into the next region
+DEV void rp_dep(float v) { asm volatile("" ::"v"(v)); }
+template <class... T>
+DEV void rp_mark(RegionProf* p, int r, T... deps) {
   if (!p) return;
+  (rp_dep((float)deps), ...);
   const uint64_t ex = __builtin_amdgcn_read_exec();
   const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   if (lane == __builtin_ffsll((long long)ex) - 1) {
@@ -68,7 +73,8 @@ DEV void rp_mark(RegionProf* p, int r) {
 }
 #else
 struct RegionProf {};
-DEV void rp_mark(RegionProf*, int) {}
+template <class... T>
+DEV void rp_mark(RegionProf*, int, T...) {}
 #endif
 
 struct EnvState {
@@ -359,7 +365,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
     aabb(B, b0x, b0y, b1x, b1y);
     ov = mnx < b1x && mxx > b0x && mny < b1y && mxy > b0y;
   }
-  rp_mark(rp, RP_AABB_LL + EVK);
+  rp_mark(rp, RP_AABB_LL + EVK, ov ? 1.0f : 0.0f);
   DUP(1, { const auto Ap = perturbed(A); sink(aabb_overlap(Ap, B) ? 1.0f : 0.0f); });
   if (!ov) return;
   if (ec) ec[EV_AABB_LL + EVK]++;
@@ -381,7 +387,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   else if constexpr (FLAT) hit = sat_floor<NA, NA == 6>(A, B, mnx, mny, mxx, mxy, n, depth, &axa);
   else if constexpr (KEEP) hit = sat<NA, NB, false, true>(A, B, n, depth, &axa, &axb);
   else hit = sat<NA, NB, GENERIC, true>(A, B, n, depth);
-  rp_mark(rp, RP_SAT_LL + EVK);
+  rp_mark(rp, RP_SAT_LL + EVK, depth, n.x, n.y, hit ? 1.0f : 0.0f);
   DUP(2, { const auto Ap = perturbed(A); V2 n2; float d2;
            const bool h2 = sat(Ap, B, n2, d2); sink(n2.x); sink(n2.y); sink(d2); sink(h2 ? 1.0f : 0.0f); });
   if (!hit) return;
@@ -392,7 +398,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   else if constexpr (KEEP && FLAT) nc = contact_points_floor<NA, FS>(A, axa, n, c0, c1, frec);
   else if constexpr (KEEP) nc = contact_points_ax<NA, NB, FS>(A, axa, B, axb, n, c0, c1, frec);
   else nc = contact_points<NA, NB, GENERIC>(A, B, n, c0, c1);
-  rp_mark(rp, RP_CON_LL + EVK);
+  rp_mark(rp, RP_CON_LL + EVK, c0.x, c0.y, c1.x, c1.y, (float)nc);
   DUP(3, { const auto Ap = perturbed(A); V2 e0, e1;
            const int k2 = contact_points(Ap, B, n, e0, e1); sink(e0.x); sink(e1.y); sink((float)k2); });
   if (TRACE && tr && pi >= 0) {
@@ -439,7 +445,7 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   if (TRACE && tr && pi >= 0) { tr->impulse[pi][0] = j; tr->impulse[pi][1] = jf; }
   apply_impulses<BSTATIC>(bA, bB, n, j, rA, rB);
   apply_impulses<BSTATIC>(bA, bB, tangent, jf, rAF, rBF);
-  rp_mark(rp, RP_IMP_LL + EVK);
+  rp_mark(rp, RP_IMP_LL + EVK, dA.vx, dA.vy, dA.w, dB.vx, dB.vy, dB.w);
   DUP(4, { Dyn dA2 = dA, dB2 = dB; const float z = opaque_zero();
            Body cA{A.cx + z, A.cy, &dA2, mA.im, mA.ii}; Body cB{B.cx, B.cy, &dB2, mB.im, mB.ii};
            V2 sA, sB, sAF, sBF;
@@ -1036,13 +1042,13 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
   if (side == 1) joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.up, s.dup, mp, tr, 1);
   bcast_torso<0xF5>(s.body, s.dbody);
   joint_step<6, 6, 2, 3, TRACE>(s.up, s.dup, mp, s.lo, s.dlo, mp, tr, 2 + side);
-  rp_mark(rp, RP_JOINT);
+  rp_mark(rp, RP_JOINT, s.dup.w, s.dlo.w, s.up.x[0], s.lo.x[0], s.dbody.w, s.body.x[0]);
   // this leg's RigidBody.Step calls (lower then upper); a segment's two candidates run
   // floor-first after a reset, floor-last in episode 0: three slots keep a wave with
   // both kinds of walkers at three pair evaluations instead of four
   const int pb = side ? 5 : 0;
   integrate(s.lo, s.dlo, dt, adx, ady);
-  rp_mark(rp, RP_INTEG);
+  rp_mark(rp, RP_INTEG, s.lo.x[0], s.lo.y[3], s.lo.x[5], s.dlo.th);
   DUP(6, { auto l2 = perturbed(s.lo); Dyn d2 = s.dlo; integrate(l2, d2, dt, adx, ady);
            sink(l2.x[0]); sink(l2.y[5]); sink(d2.th); });
 #pragma unroll
@@ -1055,7 +1061,7 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
     rp_mark(rp, RP_OTHER);
   }
   integrate(s.up, s.dup, dt, adx, ady);
-  rp_mark(rp, RP_INTEG);
+  rp_mark(rp, RP_INTEG, s.up.x[0], s.up.y[3], s.up.x[5], s.dup.th);
 #pragma unroll
   for (int q = 0; q < 3; q++) {
     if (q == 1) resolve_pair<6, 6, false, TRACE, 1, false, Q, FS>(s.up, s.dup, mp, s.lo, s.dlo, mp, s.cup, tr, pb + 2, half, rp, nullptr, frec);
@@ -1067,7 +1073,7 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
   }
   // the torso's step, replicated in both lanes (traced by the left lane)
   integrate(s.body, s.dbody, dt, adx, ady);
-  rp_mark(rp, RP_INTEG);
+  rp_mark(rp, RP_INTEG, s.body.x[0], s.body.y[3], s.dbody.th);
   if constexpr (ROUGH) floor_pairs<5, TRACE, 1, true, TS>(s.body, s.dbody, mb, s.cbody, side == 0 ? tr : nullptr, 4, 0, ter);
   else resolve_pair<5, 4, true, TRACE, 1>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody,
                                           side == 0 ? tr : nullptr, 4, 0, rp);
@@ -1077,6 +1083,289 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
 DEV bool side_finite(const SideState& s) {  // this side's legs and the torso (see state_finite)
   const float acc = nonfinite_acc(s.lo, s.dlo) + nonfinite_acc(s.up, s.dup) + nonfinite_acc(s.body, s.dbody);
   return acc == 0.0f;
+}
+
+// ---------------- block-pooled contact stages (pair mapping, flat floor; round 5) ----------------
+// The wave-level region probe (profiles/r05_region_prof.txt) put half of a pair-mapping wave's
+// time into the leg pairs' narrow-phase tails, run wave-wide for a few lanes: per wave-substep the
+// leg-leg contact clipping + impulses 22 % of the time at 17.9 of 64 lanes, the leg-floor SAT +
+// contacts + impulses 16 % at 15.4 lanes.  A pooled stage compacts those tails over the block's
+// four waves (RigidBody.cs:66-96 / ContactPoints.cs:13-53 / Impulses.cs:12-28, unchanged order):
+// every lane decides its own candidate (bounding box, and for leg-leg the SAT: dense), the lanes
+// that go on write their pair as a task into an LDS queue -- a wave ballot + prefix (mbcnt) for the
+// slot within the wave and one LDS atomic per wave for the wave's base -- one block barrier, then
+// the queue's tasks are processed densely by as few waves as they fill (task t by lane t % 64 of
+// wave (t / 64 + rot) % 4: ~72 leg-leg tasks take two waves instead of four, ~60 floor tasks one),
+// a second barrier, and every owner reads its result back by its slot.  A task is a pure function
+// of its inputs, so whichever lane computes it the results are the owner's own bits.
+// The 36-KB region is shared over an env-step: [0, 1536) float4 the legs parked across the policy
+// ([record][lane]), [1536, 2304) the policy's observation tiles; during the substeps the task
+// queues (floor: 7 float4 per task, leg-leg: 17) below RES and both queues' results (2 float4 per
+// task) from RES.  Tasks and results live in disjoint parts, so a stage's puts never meet the
+// previous stage's late result reads; a block barrier before and after the policy section keeps
+// the stash / tiles apart from the queues.
+#ifndef WK_POOL
+#define WK_POOL 1
+#endif
+namespace pool {
+enum : int {
+  F4 = 2304,            // float4s of the region (36 KB)
+  STASH = 0, POL = 1536, RES = 1792,
+  FT = 7, FCAP = 256,   // floor tasks in [0, 1792)
+  LT = 17, LCAP = 105   // leg-leg tasks in [0, 1785)
+};
+static_assert(FT * FCAP <= RES && LT * LCAP <= RES && RES + 2 * FCAP <= F4, "queue layout");
+}  // namespace pool
+
+// One pooled stage: block-collective (every thread of the block calls it from converged code).
+// cnt: two LDS counters used alternately by consecutive stages (a stage clears the next one's
+// after its first barrier, when every reader of that counter's last use has passed).
+template <int TS, int CAP, class PUT, class WORK, class GET>
+DEV void pool_run(bool need, float4* __restrict__ q, int* cnt, uint32_t& seq, PUT&& put, WORK&& work,
+                  GET&& get) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t bal = __ballot(need);
+  int* const c = cnt + (seq & 1u);
+  int base = 0;
+  if (bal != 0ull) {  // wave-uniform: one LDS atomic per wave reserves its slots
+    int got = 0;
+    if (lane == 0) got = atomicAdd(c, __builtin_popcountll(bal));
+    base = __builtin_amdgcn_readfirstlane(got);
+  }
+  const int idx = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+  if (need && idx < CAP) put(q + idx * TS);
+  __syncthreads();
+  const int total = *(volatile int*)c;
+  if (threadIdx.x == 0) cnt[(seq + 1u) & 1u] = 0;
+  const int rot = (int)((seq + blockIdx.x) & 3u);
+  seq++;
+  if (total == 0) return;  // block-uniform
+  const int t = (((wave + rot) & 3) << 6) | lane;  // this lane's slot as a worker
+  for (int done = 0;;) {
+    const int m = total - done < CAP ? total - done : CAP;
+    if (t < m) work(q + t * TS, q + pool::RES + 2 * t);
+    __syncthreads();
+    if (need && idx >= done && idx < done + CAP) get(q + pool::RES + 2 * (idx - done));
+    done += CAP;
+    if (done >= total) break;
+    __syncthreads();  // (overflow round) every result read before the next round reuses the slots
+    if (need && idx >= done && idx < done + CAP) put(q + (idx - done) * TS);
+    __syncthreads();
+  }
+}
+
+// RigidBody.ResolveCollisions' impulse tail (Impulses.cs:12-28) on a pair whose MoveObjects has
+// run (post-correction centroids), as resolve_pair's H = 1 path
+template <bool BSTATIC>
+DEV void pair_impulses(float acx, float acy, Dyn& dA, const Mat& mA, float bcx, float bcy, Dyn& dB,
+                       const Mat& mB, V2 n, int nc, V2 c0, V2 c1) {
+  const float e = net_maxf(mA.e, mB.e);
+  const float mu = net_minf(mA.mu, mB.mu);
+  const V2 contact = nc == 2 ? vdiv(vadd(c0, c1), 2.0f) : c0;
+  Body bA{acx, acy, &dA, mA.im, mA.ii};
+  Body bB{bcx, bcy, &dB, mB.im, mB.ii};
+  V2 rA, rB, rAF, rBF;
+  const V2 tangent = mk(-n.y, n.x);
+  const float j = calc_impulse(bA, bB, contact, 1.0f + e, n, rA, rB);
+  const float jf = calc_impulse(bA, bB, contact, mu, tangent, rAF, rBF);
+  apply_impulses<BSTATIC>(bA, bB, n, j, rA, rB);
+  apply_impulses<BSTATIC>(bA, bB, tangent, jf, rAF, rBF);
+}
+
+DEV void put_poly6(float4* q, const Poly<6>& A) {
+  q[0] = make_float4(A.x[0], A.x[1], A.x[2], A.x[3]);
+  q[1] = make_float4(A.x[4], A.x[5], A.y[0], A.y[1]);
+  q[2] = make_float4(A.y[2], A.y[3], A.y[4], A.y[5]);
+}
+DEV void get_poly6(const float4* q, Poly<6>& A) {
+  const float4 a = q[0], b = q[1], c = q[2];
+  A.x[0] = a.x; A.x[1] = a.y; A.x[2] = a.z; A.x[3] = a.w;
+  A.x[4] = b.x; A.x[5] = b.y; A.y[0] = b.z; A.y[1] = b.w;
+  A.y[2] = c.x; A.y[3] = c.y; A.y[4] = c.z; A.y[5] = c.w;
+}
+DEV void put_axes6(float4* q, const EdgeAxes<6>& X) {
+  q[0] = make_float4(X.x[0], X.x[1], X.x[2], X.x[3]);
+  q[1] = make_float4(X.x[4], X.x[5], X.y[0], X.y[1]);
+  q[2] = make_float4(X.y[2], X.y[3], X.y[4], X.y[5]);
+}
+DEV void get_axes6(const float4* q, EdgeAxes<6>& X) {
+  const float4 a = q[0], b = q[1], c = q[2];
+  X.x[0] = a.x; X.x[1] = a.y; X.x[2] = a.z; X.x[3] = a.w;
+  X.x[4] = b.x; X.x[5] = b.y; X.y[0] = b.z; X.y[1] = b.w;
+  X.y[2] = c.x; X.y[3] = c.y; X.y[4] = c.z; X.y[5] = c.w;
+}
+
+// leg segment vs the flat floor, after its bounding box overlapped (the owner set Collided):
+// sat_floor, contact_points_floor, MoveObjects, impulses -- resolve_pair<6, 4, true, ...>'s tail.
+// Result: the MoveObjects translation (applied by the owner iff the SAT hit) and the new velocities.
+DEV void floor_task_put(float4* q, const Poly<6>& A, const Dyn& d, const Mat& m, float mnx, float mny,
+                        float mxx, float mxy) {
+  put_poly6(q, A);
+  q[3] = make_float4(A.cx, A.cy, d.vx, d.vy);
+  q[4] = make_float4(d.w, m.im, m.ii, m.e);
+  q[5] = make_float4(m.mu, mnx, mny, mxx);
+  q[6] = make_float4(mxy, 0.0f, 0.0f, 0.0f);
+}
+DEV void floor_task_work(const float4* q, float4* r) {
+  Poly<6> A;
+  get_poly6(q, A);
+  const float4 q3 = q[3], q4 = q[4], q5 = q[5], q6 = q[6];
+  A.cx = q3.x; A.cy = q3.y;
+  Dyn d;
+  d.vx = q3.z; d.vy = q3.w; d.w = q4.x; d.th = 0.0f;
+  const Mat m{q4.y, q4.z, q4.w, q5.x};
+  Poly<4> fl;
+  floor_poly(fl);
+  V2 n;
+  float depth;
+  EdgeAxes<6> axa;
+  const bool hit = sat_floor<6, true>(A, fl, q5.y, q5.z, q5.w, q6.x, n, depth, &axa);
+  V2 mv = mk(0.0f, 0.0f);
+  if (hit) {
+    V2 c0, c1;
+    const int nc = contact_points_floor<6>(A, axa, n, c0, c1);
+    mv = vmul(n, depth);
+    const float cx = A.cx + mv.x, cy = A.cy + mv.y;  // Skeleton.Move's centroid
+    if (nc > 0) {
+      Dyn dfl;
+      zero_dyn(dfl);
+      const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};
+      pair_impulses<true>(cx, cy, d, m, fl.cx, fl.cy, dfl, mf, n, nc, c0, c1);
+    }
+  }
+  r[0] = make_float4(mv.x, mv.y, d.vx, d.vy);
+  r[1] = make_float4(d.w, hit ? 1.0f : 0.0f, 0.0f, 0.0f);
+}
+
+// leg segment A vs the other segment B of the same leg after the SAT hit (the owner ran AABB +
+// SAT and applies MoveObjects itself): contact_points_ax from the SAT's axes, then the impulses
+// on the post-correction centroids.  Result: both segments' new velocities.
+DEV void ll_task_put(float4* q, const Poly<6>& A, const Poly<6>& B, const EdgeAxes<6>& axa,
+                     const EdgeAxes<6>& axb, V2 n, float depth, const Dyn& dA, const Dyn& dB,
+                     const Mat& m) {
+  put_poly6(q, A);
+  q[3] = make_float4(A.cx, A.cy, B.cx, B.cy);
+  put_poly6(q + 4, B);
+  put_axes6(q + 7, axa);
+  put_axes6(q + 10, axb);
+  q[13] = make_float4(n.x, n.y, depth, m.im);
+  q[14] = make_float4(dA.vx, dA.vy, dA.w, m.ii);
+  q[15] = make_float4(dB.vx, dB.vy, dB.w, m.e);
+  q[16] = make_float4(m.mu, 0.0f, 0.0f, 0.0f);
+}
+DEV void ll_task_work(const float4* q, float4* r) {
+  Poly<6> A, B;
+  get_poly6(q, A);
+  get_poly6(q + 4, B);
+  const float4 q3 = q[3], q13 = q[13], q14 = q[14], q15 = q[15], q16 = q[16];
+  A.cx = q3.x; A.cy = q3.y; B.cx = q3.z; B.cy = q3.w;
+  EdgeAxes<6> axa, axb;
+  get_axes6(q + 7, axa);
+  get_axes6(q + 10, axb);
+  const V2 n = mk(q13.x, q13.y);
+  const float depth = q13.z;
+  const Mat m{q13.w, q14.w, q15.w, q16.x};
+  Dyn dA, dB;
+  dA.vx = q14.x; dA.vy = q14.y; dA.w = q14.z; dA.th = 0.0f;
+  dB.vx = q15.x; dB.vy = q15.y; dB.w = q15.z; dB.th = 0.0f;
+  V2 c0, c1;
+  const int nc = contact_points_ax<6, 6>(A, axa, B, axb, n, c0, c1);
+  if (nc > 0) {
+    const V2 tA = vdiv(vmul(n, depth), 2.0f), tB = vdiv(vmul(vneg(n), depth), 2.0f);
+    pair_impulses<false>(A.cx + tA.x, A.cy + tA.y, dA, m, B.cx + tB.x, B.cy + tB.y, dB, m, n, nc, c0, c1);
+  }
+  r[0] = make_float4(dA.vx, dA.vy, dA.w, dB.vx);
+  r[1] = make_float4(dB.vy, dB.w, 0.0f, 0.0f);
+}
+
+struct PoolCtx {
+  float4* q;        // the block's region
+  int* cnt;         // two LDS counters
+  uint32_t seq;     // stages so far (block-uniform)
+  bool blk_post;    // some walker of the block is past its first episode (floor-first slot)
+  bool blk_ep0;     // some walker of the block is in its first episode (floor-last slot)
+};
+
+// one floor candidate slot of a leg segment, pooled; mine: this walker takes the floor in this slot
+DEV void floor_stage(Poly<6>& A, Dyn& dA, bool& colA, const Mat& m, bool mine, PoolCtx& pc,
+                     RegionProf* rp) {
+  float mnx, mny, mxx, mxy;
+  aabb(A, mnx, mny, mxx, mxy);
+  const bool ov = mine && mnx < 1050.0f && mxx > -50.0f && mny < 1050.0f && mxy > 900.0f;
+  if (ov) colA = true;  // body._isFloor -> Collided = true at the bounding box (:75)
+  rp_mark(rp, RP_AABB_LF, ov ? 1.0f : 0.0f);
+  pool_run<pool::FT, pool::FCAP>(
+      ov, pc.q, pc.cnt, pc.seq, [&](float4* t) { floor_task_put(t, A, dA, m, mnx, mny, mxx, mxy); },
+      floor_task_work,
+      [&](const float4* r) {
+        const float4 r0 = r[0], r1 = r[1];
+        if (r1.y != 0.0f) move(A, mk(r0.x, r0.y));
+        dA.vx = r0.z; dA.vy = r0.w; dA.w = r1.x;
+      });
+  rp_mark(rp, RP_CON_LF, dA.vx, dA.w);
+}
+
+// the leg-leg candidate of segment A against segment B (A's own list step), pooled after the SAT
+DEV void ll_stage(Poly<6>& A, Dyn& dA, Poly<6>& B, Dyn& dB, const Mat& m, PoolCtx& pc, RegionProf* rp) {
+  float a0x, a0y, a1x, a1y, b0x, b0y, b1x, b1y;
+  aabb(A, a0x, a0y, a1x, a1y);
+  aabb(B, b0x, b0y, b1x, b1y);
+  const bool ov = a0x < b1x && a1x > b0x && a0y < b1y && a1y > b0y;
+  rp_mark(rp, RP_AABB_LL, ov ? 1.0f : 0.0f);
+  V2 n = mk(0.0f, 0.0f);
+  float depth = 0.0f;
+  EdgeAxes<6> axa, axb;
+  bool hit = false;
+  if (ov) hit = sat<6, 6, false, true>(A, B, n, depth, &axa, &axb);
+  rp_mark(rp, RP_SAT_LL, depth, n.x, n.y, hit ? 1.0f : 0.0f);
+  pool_run<pool::LT, pool::LCAP>(
+      hit, pc.q, pc.cnt, pc.seq,
+      [&](float4* t) {
+        ll_task_put(t, A, B, axa, axb, n, depth, dA, dB, m);
+        move(A, vdiv(vmul(n, depth), 2.0f));  // MoveObjects (:99-113): both segments move
+        move(B, vdiv(vmul(vneg(n), depth), 2.0f));
+      },
+      ll_task_work,
+      [&](const float4* r) {
+        const float4 r0 = r[0], r1 = r[1];
+        dA.vx = r0.x; dA.vy = r0.y; dA.w = r0.z;
+        dB.vx = r0.w; dB.vy = r1.x; dB.w = r1.y;
+      });
+  rp_mark(rp, RP_CON_LL, dA.vx, dA.w, dB.w);
+}
+
+// substep_side for the pair mapping with the pooled stages (no traces: the TRACE kernels keep the
+// per-lane path); every slot runs in block-uniform control flow
+DEV void substep_pool(SideState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
+                      int side, PoolCtx& pc, RegionProf* rp) {
+  rp_mark(rp, RP_OTHER);
+  Poly<4> fl;
+  floor_poly(fl);
+  Dyn dfl;
+  zero_dyn(dfl);
+  const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};
+  if (side == 0) joint_step<5, 6, 1, 4, false>(s.body, s.dbody, mb, s.up, s.dup, mp, nullptr, 0);
+  bcast_torso<0xA0>(s.body, s.dbody);
+  if (side == 1) joint_step<5, 6, 1, 4, false>(s.body, s.dbody, mb, s.up, s.dup, mp, nullptr, 1);
+  bcast_torso<0xF5>(s.body, s.dbody);
+  joint_step<6, 6, 2, 3, false>(s.up, s.dup, mp, s.lo, s.dlo, mp, nullptr, 2 + side);
+  rp_mark(rp, RP_JOINT, s.dup.w, s.dlo.w, s.up.x[0], s.lo.x[0], s.dbody.w, s.body.x[0]);
+  integrate(s.lo, s.dlo, dt, adx, ady);
+  rp_mark(rp, RP_INTEG, s.lo.x[0], s.lo.y[3], s.lo.x[5], s.dlo.th);
+  // [floor if post], other segment, [floor if episode 0] (RigidBody.cs:66-96 list order)
+  if (pc.blk_post) floor_stage(s.lo, s.dlo, s.clo, mp, s.post, pc, rp);
+  ll_stage(s.lo, s.dlo, s.up, s.dup, mp, pc, rp);
+  if (pc.blk_ep0) floor_stage(s.lo, s.dlo, s.clo, mp, !s.post, pc, rp);
+  integrate(s.up, s.dup, dt, adx, ady);
+  rp_mark(rp, RP_INTEG, s.up.x[0], s.up.y[3], s.up.x[5], s.dup.th);
+  if (pc.blk_post) floor_stage(s.up, s.dup, s.cup, mp, s.post, pc, rp);
+  ll_stage(s.up, s.dup, s.lo, s.dlo, mp, pc, rp);
+  if (pc.blk_ep0) floor_stage(s.up, s.dup, s.cup, mp, !s.post, pc, rp);
+  integrate(s.body, s.dbody, dt, adx, ady);
+  rp_mark(rp, RP_INTEG, s.body.x[0], s.body.y[3], s.dbody.th);
+  resolve_pair<5, 4, true, false, 1>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody, nullptr, 4, 0, rp);
+  rp_mark(rp, RP_OTHER);
 }
 
 // PPOAgent.SampleActions / GetValueEstimate forward passes (NeuralNetwork.FeedForward,
@@ -1237,8 +1526,14 @@ void k_env_side(EnvParams P, StepArgs A) {
   const int slot = eraw < n ? eraw : n - 1;
   const int e = A.order ? A.order[slot] : slot;
   const bool leader = side == 0 && half == 0 && active;
-  __shared__ float pol_lds[POLICY ? (SIDE_BLOCK / 64) * 768 : 1];
+  // POOL: the pooled contact stages (pair mapping, flat floor, no traces); their 36-KB region
+  // also holds the policy tiles and the legs' stash, so pol_lds / face_lds shrink to nothing
+  constexpr bool POOL = WK_POOL && Q == 1 && !ROUGH && !TRACE;
+  static_assert(!POOL || SIDE_BLOCK == 256, "the pool layout is for 4-wave blocks");
+  __shared__ float pol_lds[POLICY && !POOL ? (SIDE_BLOCK / 64) * 768 : 1];
   __shared__ float wz_lds[POLICY ? mf::WEND : 1];  // operand-order weights (41 KB, 2 blocks/CU)
+  __shared__ float4 pool_lds[POOL ? pool::F4 : 1];
+  __shared__ int pool_cnt[2];
   // RoughFloor: the walker's terrain heights 800 + Random.Next(0, 100) (Environment.cs:242-250),
   // [draw][walker of block]; the walker's lanes write the same values and read only its column
   constexpr int WPB = SIDE_BLOCK >> SH;
@@ -1246,9 +1541,16 @@ void k_env_side(EnvParams P, StepArgs A) {
   // the pair mapping's contact faces (significant_face_lds): 6 float4 records per lane,
   // [record][lane of block] (24 KB per block; 2 blocks of 77 KB fit a CU's 160 KB -- not with the
   // rough floor's terrain as well, which would leave one block per CU)
-  constexpr int FS = ((Q == 1 && !ROUGH) || (Q == 2 && WK_FACE_LDS_QUAD)) && WK_FACE_LDS ? SIDE_BLOCK : 0;
+  constexpr int FS = !POOL && (((Q == 1 && !ROUGH) || (Q == 2 && WK_FACE_LDS_QUAD)) && WK_FACE_LDS) ? SIDE_BLOCK : 0;
   __shared__ float4 face_lds[FS ? 6 * SIDE_BLOCK : 1];
   float4* const frec = face_lds + (FS ? threadIdx.x : 0);
+  // the legs' stash across the policy section: the face column, or the pool region's first part
+  constexpr int SS = POOL ? SIDE_BLOCK : FS;
+  float4* const stash = POOL ? pool_lds + (pool::STASH + threadIdx.x) : frec;
+  PoolCtx pc{pool_lds, pool_cnt, 0u, true, true};
+  if constexpr (POOL) {
+    if (threadIdx.x < 2) pool_cnt[threadIdx.x] = 0;  // (read after the stages' first barrier)
+  }
   const int wib = ((threadIdx.x >> 6) * wpw) + ((threadIdx.x & ((wpw << SH) - 1)) >> SH);
   const float* const ter = ter_lds + wib;
   if constexpr (ROUGH) {
@@ -1261,7 +1563,7 @@ void k_env_side(EnvParams P, StepArgs A) {
       ((pf4*)wz_lds)[i] = ((const pf4*)A.Wz)[i];
     __syncthreads();
   }
-  float* const wave_pol = pol_lds + (POLICY ? (threadIdx.x >> 6) * 768 : 0);
+  float* const wave_pol = (POOL ? (float*)(pool_lds + pool::POL) : pol_lds) + (POLICY ? (threadIdx.x >> 6) * 768 : 0);
   SideState s;
   load_side(s, A.st, e, side);
   const float dx = A.dxoff[e];
@@ -1289,6 +1591,13 @@ void k_env_side(EnvParams P, StepArgs A) {
   for (int k = 0; k < A.k_steps; k++) {
     float a[4], lp[4], obs[12];
     rp_mark(rp, RP_OTHER);
+    if constexpr (POOL) {
+      // which floor slots the block's walkers take this env-step (the list order changes only
+      // at a reset); also the barrier that keeps the policy's stash / tiles from the last
+      // substep's late result reads
+      pc.blk_post = __syncthreads_or(s.post ? 1 : 0) != 0;
+      pc.blk_ep0 = __syncthreads_or(s.post ? 0 : 1) != 0;
+    }
     if (POLICY) {
       get_obs_side(s, side, obs);
       // The policy's matrix-core section needs the most registers of the loop, while the legs'
@@ -1296,8 +1605,8 @@ void k_env_side(EnvParams P, StepArgs A) {
       // face column (free outside the contact clipping) rather than leave them to the spill; the
       // empty asm with a memory clobber keeps the compiler from forwarding the parked values in
       // registers across the section.  Pure data movement: bit-identical.
-      if constexpr (FS != 0 && WK_POLICY_STASH) {
-        park_legs<FS>(s, frec);
+      if constexpr (SS != 0 && WK_POLICY_STASH) {
+        park_legs<SS>(s, stash);
         asm volatile("" ::: "memory");
       }
       float z3[4], mean[4], v;
@@ -1318,10 +1627,11 @@ void k_env_side(EnvParams P, StepArgs A) {
         st_nt4(A.traj_lp + row * 4 + eo * 4u, lp[0], lp[1], lp[2], lp[3]);
         __builtin_nontemporal_store(v, A.traj_v + row + eo);
       }
-      if constexpr (FS != 0 && WK_POLICY_STASH) {
+      if constexpr (SS != 0 && WK_POLICY_STASH) {
         asm volatile("" ::: "memory");
-        unpark_legs<FS>(s, frec);
+        unpark_legs<SS>(s, stash);
       }
+      if constexpr (POOL) __syncthreads();  // stash and tiles read before the queues reuse them
     } else {
 #pragma unroll
       for (int d = 0; d < 4; d++) a[d] = A.actions[((size_t)k * n + e) * 4 + d];
@@ -1336,8 +1646,12 @@ void k_env_side(EnvParams P, StepArgs A) {
     }
 #pragma unroll 1
     for (int it = 0; it < P.iterations; it++) {
-      PairTraceDev* tr = (TRACE && active && half == 0) ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
-      substep_side<TRACE, Q, ROUGH, WPB, FS>(s, mp, mb, dt, adx, ady, tr, side, half, rp, ter, frec);
+      if constexpr (POOL) {
+        substep_pool(s, mp, mb, dt, adx, ady, side, pc, rp);
+      } else {
+        PairTraceDev* tr = (TRACE && active && half == 0) ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
+        substep_side<TRACE, Q, ROUGH, WPB, FS>(s, mp, mb, dt, adx, ady, tr, side, half, rp, ter, frec);
+      }
     }
     // Walker.Update + terminal flags (both upper legs and the torso)
     s.prevx = s.posx; s.prevy = s.posy;
