@@ -37,6 +37,11 @@ enum ProfKind { PK_PHYS = 0, PK_GRAD, PK_REDUCE, PK_ADAM, PK_ALLRED, PK_RET, PK_
 struct wk_ctx {
   wk_config cfg;
   int grad_impl = -1;  // matrix-core gradient kernel (wk::GI_*; -1 = by minibatch size)
+  bool grad_tail = true;  // single-GPU minibatch tail fused into the gradient kernel (WK_GRAD_TAIL)
+  uint32_t* tail_cnt = nullptr;  // device: [0] block-arrival counter, [1] bounded-wait error
+  uint32_t tail_seq = 0;         // the counter's value after the last fused launch
+  bool tail_used = false;        // a fused launch ran since the last error check
+  int n_cu = 0;                  // compute units of the device (the fused tail needs every block resident)
   int device = 0;
   int n = 0;
   uint64_t seed = 0;
@@ -309,6 +314,9 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   // per device; wk_create is the only place, so launches never race on it)
   if (wk::configure_device_kernels() != hipSuccess) { x->err = "hipFuncSetAttribute failed"; return fail(WK_ERR_HIP); }
   x->grad_impl = wk::grad_impl_env();
+  if (const char* e = getenv("WK_GRAD_TAIL")) x->grad_tail = atoi(e) != 0;
+  if (hipDeviceGetAttribute(&x->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    x->n_cu = 0;  // (no fused tail then)
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) {
     x->err = "hipStreamCreate failed";
     return fail(WK_ERR_HIP);
@@ -366,6 +374,7 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   ALLOC(x->m, sizeof(float) * wk::NPARAM);
   ALLOC(x->v, sizeof(float) * wk::NPARAM);
   ALLOC(x->grad, sizeof(float) * wk::SLAB);
+  ALLOC(x->tail_cnt, 2 * sizeof(uint32_t));
   ALLOC(x->ts, sizeof(float) * 12 * n * T);
   ALLOC(x->ta, sizeof(float) * 4 * n * T);
   ALLOC(x->tlp, sizeof(float) * 4 * n * T);
@@ -403,6 +412,7 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
       hipMemcpy(x->mat, mt.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(x->rng_t, 0, sizeof(uint32_t) * n) != hipSuccess ||
       hipMemset(x->m, 0, sizeof(float) * wk::NPARAM) != hipSuccess ||
+      hipMemset(x->tail_cnt, 0, 2 * sizeof(uint32_t)) != hipSuccess ||
       hipMemset(x->v, 0, sizeof(float) * wk::NPARAM) != hipSuccess ||
       hipMemset(x->td, 0, n * T) != hipSuccess ||
       hipMemset(x->ep_acc, 0, sizeof(double) * n) != hipSuccess ||
@@ -437,7 +447,7 @@ int wk_destroy(wk_ctx* c) {
   void* bufs[] = {c->st, c->dxoff, c->mat, c->rng_t, c->W, c->Wz, c->m, c->v, c->grad, c->ts, c->ta,
                   c->tlp, c->tr, c->tv, c->tret, c->tadv, c->td, c->partial, c->scratch, c->scratch2,
                   c->ep_acc, c->ep_len, c->ep_scratch, c->ep_rowcnt, c->ep_count, c->ep_log,
-                  c->loss_log, c->props, c->snap, c->counts, c->order, c->order_cnt};
+                  c->loss_log, c->props, c->snap, c->counts, c->order, c->order_cnt, c->tail_cnt};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -445,11 +455,27 @@ int wk_destroy(wk_ctx* c) {
   return WK_OK;
 }
 
+// the fused minibatch tail's bounded wait ran out (never in a sound launch: every block of the
+// launch is resident) -- reported at the next synchronising call
+static int tail_status(wk_ctx* c) {
+  if (!c->tail_used) return WK_OK;
+  uint32_t err = 0;
+  HIPCHK(c, hipMemcpyAsync(&err, c->tail_cnt + 1, sizeof err, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->tail_used = false;
+  if (err) {
+    SETERR(c, "fused minibatch tail: a tail block's wait for the gradient launch's blocks ran out "
+           "(some Adam steps incomplete)");
+    return WK_ERR_HIP;
+  }
+  return WK_OK;
+}
+
 int wk_sync(wk_ctx* c) {
   DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  return WK_OK;
+  return tail_status(c);
 }
 
 int wk_num_envs(const wk_ctx* c) { return c ? c->n : 0; }
@@ -1028,11 +1054,6 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
     c->partial_floats = need;
   }
   g.partial = c->partial;
-  {
-    ProfScope ps(c, PK_GRAD, 0, 2);
-    HIPCHK(c, wpb == 0 ? wk::launch_ppo_grad_mfma(g, nblocks, gi, c->stream)
-                       : wk::launch_ppo_grad(g, wpb, nblocks, c->stream));
-  }
   wk::AdamArgs a{};
   if (apply_adam) {
     c->adam_t += 1;
@@ -1051,6 +1072,26 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   // with a communicator (any size, also one rank) the collective path runs: reduction,
   // RCCL all-reduce, Adam -- a single-GPU test then covers the multi-GPU sequence
   const bool multi = c->comm != nullptr || c->host_ar != nullptr || c->ipc;
+  // one GPU, Adam, a matrix-core kernel with a tail (ws / tp / tp1), every block resident at
+  // once (at most one per CU): the ordered reduction + Adam run in the gradient launch's last
+  // blocks (wk_tail.h grad_tail) -- the same association, one launch per minibatch
+  const bool fused = apply_adam && !multi && wpb == 0 && gi != wk::GI_MF && c->grad_tail &&
+                     nblocks <= 256 && nblocks <= c->n_cu;  // (RG x RG slabs: one-launch form)
+  if (fused) {
+    c->tail_used = true;
+    c->tail_seq += (uint32_t)nblocks;
+    g.tail.on = 1;
+    g.tail.cnt = c->tail_cnt;
+    g.tail.err = c->tail_cnt + 1;
+    g.tail.target = c->tail_seq;
+    g.tail.grad = c->grad;
+    g.tail.a = a;
+  }
+  {
+    ProfScope ps(c, PK_GRAD, 0, 2);
+    HIPCHK(c, wpb == 0 ? wk::launch_ppo_grad_mfma(g, nblocks, gi, c->stream)
+                       : wk::launch_ppo_grad(g, wpb, nblocks, c->stream));
+  }
   // reduction, exchange and Adam in one launch (k_reduce_xch_adam); a gradient-only call
   // (apply_adam 0: a.W == null) runs the exchange alone, so on every kind of context the
   // returned gradient is the sum over the ranks
@@ -1069,6 +1110,7 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
     return WK_OK;
   }
   if (apply_adam && !multi) {  // one GPU: the last reduction stage applies Adam
+    if (fused) return WK_OK;     // (done by the gradient kernel's last blocks)
     ProfScope ps(c, PK_REDUCE, 0, 2);
     HIPCHK(c, wk::launch_grad_reduce_adam(c->partial, nblocks, part2, c->grad, a, c->stream));
     return WK_OK;
@@ -1273,6 +1315,7 @@ int wk_ppo_update(wk_ctx* c, const wk_ppo_args* args, float* critic_diag, float*
   float diag[3] = {0, 0, 0};
   HIPCHK(c, hipMemcpyAsync(diag, c->grad + wk::NPARAM, sizeof(diag), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (int r = tail_status(c)) return r;
   if (critic_diag) *critic_diag = diag[0];
   if (actor_diag) *actor_diag = diag[1];
   return WK_OK;

@@ -76,6 +76,22 @@ struct SceneDev {
   float adx[SCENE_MAX_PROPS], ady[SCENE_MAX_PROPS];  // acceleration * deltaTime
 };
 
+struct AdamArgs {
+  float* W; float* m; float* v; const float* grad;
+  float* Wz;  // operand-order image kept in step with W (or null)
+  float c1, c2, beta1, beta2, bc1, bc2, alpha, eps;
+};
+
+// the single-GPU minibatch tail fused into the matrix-core gradient kernels (wk_tail.h grad_tail)
+struct GradTail {
+  uint32_t* cnt;     // the context's monotone block-arrival counter (device)
+  uint32_t target;   // its value once every block of this launch has arrived
+  int on;            // 0: no tail (the separate reduction launch follows)
+  float* grad;       // the summed slab
+  uint32_t* err;     // set if a tail block's bounded wait ran out
+  AdamArgs a;
+};
+
 struct GradArgs {
   const float* W;        // params
   const float* Wz;       // the same params in the matrix-core operand order (wk_mfma_layout.h)
@@ -95,12 +111,7 @@ struct GradArgs {
   float lp_const;        // -ln(std) - ln(sqrt(2 pi))
   float upper, lower;    // 1 + eps, 1 - eps
   float* partial;        // [nblocks][SLAB]
-};
-
-struct AdamArgs {
-  float* W; float* m; float* v; const float* grad;
-  float* Wz;  // operand-order image kept in step with W (or null)
-  float c1, c2, beta1, beta2, bc1, bc2, alpha, eps;
+  GradTail tail;         // (matrix-core kernels ws / tp / tp1)
 };
 
 // gradient + critic diag, actor diag, skipped, then zero pads to a multiple of 4 floats (16-byte

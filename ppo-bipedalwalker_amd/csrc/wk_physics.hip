@@ -49,7 +49,8 @@ namespace wk {
 // is only the code between regions (slot selection, joins, the env-step tail).  Each mark also
 // adds the number of active lanes, so lanes / count is the region's mean active lanes.
 enum { RP_JOINT, RP_INTEG, RP_AABB_LL, RP_AABB_LF, RP_AABB_BF, RP_SAT_LL, RP_SAT_LF, RP_SAT_BF,
-       RP_CON_LL, RP_CON_LF, RP_CON_BF, RP_IMP_LL, RP_IMP_LF, RP_IMP_BF, RP_POLICY, RP_OTHER, RP_N };
+       RP_CON_LL, RP_CON_LF, RP_CON_BF, RP_IMP_LL, RP_IMP_LF, RP_IMP_BF, RP_POLICY, RP_OTHER,
+       RP_Q_PUT, RP_Q_B1, RP_Q_WORK, RP_Q_B2, RP_Q_GET, RP_N };  // (RP_Q_*: the pooled stages)
 #ifdef WK_REGION_PROF
 static __device__ unsigned long long g_region_prof[3 * RP_N];  // ticks, lane sums, counts
 struct WaveProf { unsigned long long acc[RP_N]; unsigned long long lanes[RP_N]; unsigned cnt[RP_N]; unsigned long long t; };
@@ -1020,6 +1021,33 @@ DEV void get_obs_side(const SideState& s, int side, float o[12]) {
   o[11] = left ? otup : tup;
 }
 
+// The torso's RigidBody.Step (RigidBody.cs:54-96), replicated in every lane of the walker (traced
+// by the left lane): integrate, then its only candidate, the floor.  It reads and writes the torso
+// alone (its leg pairs are associated bodies, Walker.cs:202-209), and no leg step reads the torso,
+// so it commutes with the legs' steps that precede it in the list [LLL, LLU, Body, RLL, RLU]:
+// WK_TORSO_EARLY (default) runs it right after the joints, in the lower leg's integrate's basic
+// block, where the two independent integrate chains interleave (bit-identical either way).
+#ifndef WK_TORSO_EARLY
+#define WK_TORSO_EARLY 1
+#endif
+template <bool TRACE, bool ROUGH, int TS>
+DEV void torso_step(SideState& s, const Mat& mb, float dt, float adx, float ady, PairTraceDev* tr,
+                    int side, RegionProf* rp, const float* ter) {
+  integrate(s.body, s.dbody, dt, adx, ady);
+  rp_mark(rp, RP_INTEG, s.body.x[0], s.body.y[3], s.dbody.th);
+  if constexpr (ROUGH) {
+    floor_pairs<5, TRACE, 1, true, TS>(s.body, s.dbody, mb, s.cbody, side == 0 ? tr : nullptr, 4, 0, ter);
+  } else {
+    Poly<4> fl;
+    floor_poly(fl);
+    Dyn dfl;
+    zero_dyn(dfl);
+    const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};
+    resolve_pair<5, 4, true, TRACE, 1>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody,
+                                       side == 0 ? tr : nullptr, 4, 0, rp);
+  }
+}
+
 // ROUGH: the floor candidates are CreateRoughFloor's 10 segments (floor_pairs, general SAT /
 // contacts, replicated in both halves of the quad mapping; ter: this walker's terrain column in
 // LDS with stride TS); the leg-leg pairs keep their split
@@ -1047,6 +1075,9 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
   // floor-first after a reset, floor-last in episode 0: three slots keep a wave with
   // both kinds of walkers at three pair evaluations instead of four
   const int pb = side ? 5 : 0;
+#if WK_TORSO_EARLY
+  torso_step<TRACE, ROUGH, TS>(s, mb, dt, adx, ady, tr, side, rp, ter);
+#endif
   integrate(s.lo, s.dlo, dt, adx, ady);
   rp_mark(rp, RP_INTEG, s.lo.x[0], s.lo.y[3], s.lo.x[5], s.dlo.th);
   DUP(6, { auto l2 = perturbed(s.lo); Dyn d2 = s.dlo; integrate(l2, d2, dt, adx, ady);
@@ -1071,12 +1102,9 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
     }
     rp_mark(rp, RP_OTHER);
   }
-  // the torso's step, replicated in both lanes (traced by the left lane)
-  integrate(s.body, s.dbody, dt, adx, ady);
-  rp_mark(rp, RP_INTEG, s.body.x[0], s.body.y[3], s.dbody.th);
-  if constexpr (ROUGH) floor_pairs<5, TRACE, 1, true, TS>(s.body, s.dbody, mb, s.cbody, side == 0 ? tr : nullptr, 4, 0, ter);
-  else resolve_pair<5, 4, true, TRACE, 1>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody,
-                                          side == 0 ? tr : nullptr, 4, 0, rp);
+#if !WK_TORSO_EARLY
+  torso_step<TRACE, ROUGH, TS>(s, mb, dt, adx, ady, tr, side, rp, ter);
+#endif
   rp_mark(rp, RP_OTHER);
 }
 
@@ -1105,7 +1133,7 @@ DEV bool side_finite(const SideState& s) {  // this side's legs and the torso (s
 // previous stage's late result reads; a block barrier before and after the policy section keeps
 // the stash / tiles apart from the queues.
 #ifndef WK_POOL
-#define WK_POOL 1
+#define WK_POOL 0  // bit 0: the leg-floor slots, bit 1: the leg-leg pairs (0: the per-lane kernel)
 #endif
 namespace pool {
 enum : int {
@@ -1122,7 +1150,7 @@ static_assert(FT * FCAP <= RES && LT * LCAP <= RES && RES + 2 * FCAP <= F4, "que
 // after its first barrier, when every reader of that counter's last use has passed).
 template <int TS, int CAP, class PUT, class WORK, class GET>
 DEV void pool_run(bool need, float4* __restrict__ q, int* cnt, uint32_t& seq, PUT&& put, WORK&& work,
-                  GET&& get) {
+                  GET&& get, RegionProf* rp = nullptr) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t bal = __ballot(need);
   int* const c = cnt + (seq & 1u);
@@ -1135,8 +1163,10 @@ DEV void pool_run(bool need, float4* __restrict__ q, int* cnt, uint32_t& seq, PU
   const int idx = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
   if (need && idx < CAP) put(q + idx * TS);
+  rp_mark(rp, RP_Q_PUT);
   __syncthreads();
   const int total = *(volatile int*)c;
+  rp_mark(rp, RP_Q_B1, (float)total);
   if (threadIdx.x == 0) cnt[(seq + 1u) & 1u] = 0;
   const int rot = (int)((seq + blockIdx.x) & 3u);
   seq++;
@@ -1145,8 +1175,11 @@ DEV void pool_run(bool need, float4* __restrict__ q, int* cnt, uint32_t& seq, PU
   for (int done = 0;;) {
     const int m = total - done < CAP ? total - done : CAP;
     if (t < m) work(q + t * TS, q + pool::RES + 2 * t);
+    rp_mark(rp, RP_Q_WORK);
     __syncthreads();
+    rp_mark(rp, RP_Q_B2);
     if (need && idx >= done && idx < done + CAP) get(q + pool::RES + 2 * (idx - done));
+    rp_mark(rp, RP_Q_GET);
     done += CAP;
     if (done >= total) break;
     __syncthreads();  // (overflow round) every result read before the next round reuses the slots
@@ -1302,7 +1335,7 @@ DEV void floor_stage(Poly<6>& A, Dyn& dA, bool& colA, const Mat& m, bool mine, P
         const float4 r0 = r[0], r1 = r[1];
         if (r1.y != 0.0f) move(A, mk(r0.x, r0.y));
         dA.vx = r0.z; dA.vy = r0.w; dA.w = r1.x;
-      });
+      }, rp);
   rp_mark(rp, RP_CON_LF, dA.vx, dA.w);
 }
 
@@ -1331,40 +1364,62 @@ DEV void ll_stage(Poly<6>& A, Dyn& dA, Poly<6>& B, Dyn& dB, const Mat& m, PoolCt
         const float4 r0 = r[0], r1 = r[1];
         dA.vx = r0.x; dA.vy = r0.y; dA.w = r0.z;
         dB.vx = r0.w; dB.vy = r1.x; dB.w = r1.y;
-      });
+      }, rp);
   rp_mark(rp, RP_CON_LL, dA.vx, dA.w, dB.w);
+}
+
+// a floor slot / the leg-leg pair of a segment, pooled (WK_POOL bit 0 / bit 1) or per lane
+template <bool POOLED>
+DEV void floor_slot(Poly<6>& A, Dyn& dA, bool& colA, const Mat& m, bool mine, PoolCtx& pc,
+                    RegionProf* rp) {
+  if constexpr (POOLED) {
+    floor_stage(A, dA, colA, m, mine, pc, rp);
+  } else if (mine) {
+    Poly<4> fl;
+    floor_poly(fl);
+    Dyn dfl;
+    zero_dyn(dfl);
+    const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};
+    resolve_pair<6, 4, true, false, 1>(A, dA, m, fl, dfl, mf, colA, nullptr, -1, 0, rp);
+  }
+}
+template <bool POOLED>
+DEV void ll_slot(Poly<6>& A, Dyn& dA, bool& colA, Poly<6>& B, Dyn& dB, const Mat& m, PoolCtx& pc,
+                 RegionProf* rp) {
+  if constexpr (POOLED) ll_stage(A, dA, B, dB, m, pc, rp);
+  else resolve_pair<6, 6, false, false, 1>(A, dA, m, B, dB, m, colA, nullptr, -1, 0, rp);
 }
 
 // substep_side for the pair mapping with the pooled stages (no traces: the TRACE kernels keep the
 // per-lane path); every slot runs in block-uniform control flow
+template <int PM>  // WK_POOL: bit 0 the floor slots, bit 1 the leg-leg pairs
 DEV void substep_pool(SideState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
                       int side, PoolCtx& pc, RegionProf* rp) {
+  constexpr bool PF = (PM & 1) != 0, PL = (PM & 2) != 0;
   rp_mark(rp, RP_OTHER);
-  Poly<4> fl;
-  floor_poly(fl);
-  Dyn dfl;
-  zero_dyn(dfl);
-  const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};
   if (side == 0) joint_step<5, 6, 1, 4, false>(s.body, s.dbody, mb, s.up, s.dup, mp, nullptr, 0);
   bcast_torso<0xA0>(s.body, s.dbody);
   if (side == 1) joint_step<5, 6, 1, 4, false>(s.body, s.dbody, mb, s.up, s.dup, mp, nullptr, 1);
   bcast_torso<0xF5>(s.body, s.dbody);
   joint_step<6, 6, 2, 3, false>(s.up, s.dup, mp, s.lo, s.dlo, mp, nullptr, 2 + side);
   rp_mark(rp, RP_JOINT, s.dup.w, s.dlo.w, s.up.x[0], s.lo.x[0], s.dbody.w, s.body.x[0]);
+#if WK_TORSO_EARLY
+  torso_step<false, false, 1>(s, mb, dt, adx, ady, nullptr, side, rp, nullptr);
+#endif
   integrate(s.lo, s.dlo, dt, adx, ady);
   rp_mark(rp, RP_INTEG, s.lo.x[0], s.lo.y[3], s.lo.x[5], s.dlo.th);
   // [floor if post], other segment, [floor if episode 0] (RigidBody.cs:66-96 list order)
-  if (pc.blk_post) floor_stage(s.lo, s.dlo, s.clo, mp, s.post, pc, rp);
-  ll_stage(s.lo, s.dlo, s.up, s.dup, mp, pc, rp);
-  if (pc.blk_ep0) floor_stage(s.lo, s.dlo, s.clo, mp, !s.post, pc, rp);
+  if (pc.blk_post) floor_slot<PF>(s.lo, s.dlo, s.clo, mp, s.post, pc, rp);
+  ll_slot<PL>(s.lo, s.dlo, s.clo, s.up, s.dup, mp, pc, rp);
+  if (pc.blk_ep0) floor_slot<PF>(s.lo, s.dlo, s.clo, mp, !s.post, pc, rp);
   integrate(s.up, s.dup, dt, adx, ady);
   rp_mark(rp, RP_INTEG, s.up.x[0], s.up.y[3], s.up.x[5], s.dup.th);
-  if (pc.blk_post) floor_stage(s.up, s.dup, s.cup, mp, s.post, pc, rp);
-  ll_stage(s.up, s.dup, s.lo, s.dlo, mp, pc, rp);
-  if (pc.blk_ep0) floor_stage(s.up, s.dup, s.cup, mp, !s.post, pc, rp);
-  integrate(s.body, s.dbody, dt, adx, ady);
-  rp_mark(rp, RP_INTEG, s.body.x[0], s.body.y[3], s.dbody.th);
-  resolve_pair<5, 4, true, false, 1>(s.body, s.dbody, mb, fl, dfl, mf, s.cbody, nullptr, 4, 0, rp);
+  if (pc.blk_post) floor_slot<PF>(s.up, s.dup, s.cup, mp, s.post, pc, rp);
+  ll_slot<PL>(s.up, s.dup, s.cup, s.lo, s.dlo, mp, pc, rp);
+  if (pc.blk_ep0) floor_slot<PF>(s.up, s.dup, s.cup, mp, !s.post, pc, rp);
+#if !WK_TORSO_EARLY
+  torso_step<false, false, 1>(s, mb, dt, adx, ady, nullptr, side, rp, nullptr);
+#endif
   rp_mark(rp, RP_OTHER);
 }
 
@@ -1647,7 +1702,7 @@ void k_env_side(EnvParams P, StepArgs A) {
 #pragma unroll 1
     for (int it = 0; it < P.iterations; it++) {
       if constexpr (POOL) {
-        substep_pool(s, mp, mb, dt, adx, ady, side, pc, rp);
+        substep_pool<WK_POOL>(s, mp, mb, dt, adx, ady, side, pc, rp);
       } else {
         PairTraceDev* tr = (TRACE && active && half == 0) ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
         substep_side<TRACE, Q, ROUGH, WPB, FS>(s, mp, mb, dt, adx, ady, tr, side, half, rp, ter, frec);

@@ -15,6 +15,7 @@
 #include "wk_common.h"
 #include "wk_kernels.h"
 #include "wk_mfma_layout.h"
+#include "wk_tail.h"
 
 namespace wk {
 
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(64 * WPB) void k_ppo_grad(GradArgs g) {
 // Deterministic two-level sum of the block slabs (fixed association, no atomics):
 // stage 1 folds groups of RG consecutive slabs (all RG loads issued before the ordered
 // adds, so the chain is one memory latency, not RG); stage 2 folds the groups in order.
-enum { RG = 16 };
+// (RG, QB, adam_apply and the one-launch job: wk_tail.h)
 __global__ void k_grad_reduce1(const float* __restrict__ partial, int nblocks, float* part2) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const int g = blockIdx.y;
@@ -294,19 +295,6 @@ __global__ void k_grad_reduce2(const float* __restrict__ part2, int ngroups, flo
   grad[p] = sum_groups(part2, ngroups, p);
 }
 
-// DenseLayer.Adam (DenseLayer.cs:125-159) for one parameter, from its current m, v, w
-DEV void adam_apply(const AdamArgs& a, int p, float gr, float m0, float v0, float w0) {
-  float m = (gr * a.c1) + (m0 * a.beta1);
-  float v = (v0 * a.beta2) + ((gr * gr) * a.c2);
-  a.m[p] = m;
-  a.v[p] = v;
-  float mh = m / a.bc1;
-  float vh = v / a.bc2;
-  float den = sqrtf(vh) + a.eps;
-  const float w = w0 - ((mh / den) * a.alpha);
-  a.W[p] = w;
-  if (a.Wz) mf_scatter_param(a.Wz, p, w);
-}
 DEV void adam_param(const AdamArgs& a, int p, float gr) { adam_apply(a, p, gr, a.m[p], a.v[p], a.W[p]); }
 
 // elementwise over all 6149 parameters
@@ -326,57 +314,16 @@ __global__ void k_grad_reduce2_adam(const float* __restrict__ part2, int ngroups
 }
 
 // One-launch form of the two stages for nblocks <= RG * RG, bit-identical association
-// (RG consecutive slabs in order, then the groups in order): a block owns QB parameter
-// quads; thread (group gi, quad qi) folds its group's RG slabs with 16-byte loads (all issued
-// before the ordered adds), and the 16 group sums are folded in order through LDS.  ADAM: the
-// single-GPU tail applies Adam as well.
-#ifndef WK_REDUCE_QB
-#define WK_REDUCE_QB 16
-#endif
-enum { QB = WK_REDUCE_QB };  // parameter quads per block (RG x QB threads; 16 timed best of 4 / 8 / 16)
+// (RG consecutive slabs in order, then the groups in order): a block is one job of wk_tail.h's
+// reduce_job (QB parameter quads; thread (group gi, quad qi) folds its group's RG slabs with
+// 16-byte loads, all issued before the ordered adds, and the 16 group sums are folded in order
+// through LDS).  ADAM: the single-GPU tail applies Adam as well.
 template <bool ADAM>
 __global__ __launch_bounds__(RG * QB) void k_grad_reduce_fused(const float* __restrict__ partial,
                                                               int nblocks, float* grad, AdamArgs a) {
-  static_assert(SLAB % 4 == 0, "16-byte slab rows");
-  __shared__ float4 gs[RG][QB];
-  const int qi = threadIdx.x % QB, gi = threadIdx.x / QB;
-  const int q = blockIdx.x * QB + qi;  // parameters 4q .. 4q + 3
-  const int ngroups = (nblocks + RG - 1) / RG;
-  // the Adam operands do not depend on the reduction: their loads go out with the slab loads
-  // (one memory latency per minibatch tail instead of two)
-  const int pa = 4 * q + gi;
-  const bool adam_lane = ADAM && gi < 4 && pa < NPARAM;
-  float m0 = 0.0f, v0 = 0.0f, w0 = 0.0f;
-  if (adam_lane) { m0 = a.m[pa]; v0 = a.v[pa]; w0 = a.W[pa]; }
-  float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (q < SLAB / 4 && gi < ngroups) {
-    const int b0 = gi * RG;
-    float4 v[RG];
-#pragma unroll
-    for (int j = 0; j < RG; j++)
-      v[j] = (b0 + j < nblocks) ? ((const float4*)(partial + (size_t)(b0 + j) * SLAB))[q]
-                                : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll
-    for (int j = 0; j < RG; j++)
-      if (b0 + j < nblocks) {
-        acc.x = acc.x + v[j].x; acc.y = acc.y + v[j].y;
-        acc.z = acc.z + v[j].z; acc.w = acc.w + v[j].w;
-      }
-  }
-  gs[gi][qi] = acc;
-  __syncthreads();
-  if (gi < 4 && q < SLAB / 4) {  // one parameter per thread: component gi of quad qi
-    const float* gf = (const float*)gs;
-    const int p = 4 * q + gi;
-    float gv[RG], t = 0.0f;  // (all RG reads issued before the ordered adds)
-#pragma unroll
-    for (int g = 0; g < RG; g++) gv[g] = gf[(g * QB + qi) * 4 + gi];
-#pragma unroll
-    for (int g = 0; g < RG; g++)
-      if (g < ngroups) t = t + gv[g];
-    grad[p] = t;
-    if (adam_lane) adam_apply(a, p, t, m0, v0, w0);
-  }
+  static_assert(SLAB % 4 == 0 && RG * QB == 256, "16-byte slab rows, 256-thread jobs");
+  __shared__ float4 gs[RG * QB];
+  reduce_job<ADAM>(blockIdx.x, threadIdx.x, partial, nblocks, grad, a, gs);
 }
 
 // Normalize (PPOAgent.cs:461-472): LINQ Average/Sum accumulate in double

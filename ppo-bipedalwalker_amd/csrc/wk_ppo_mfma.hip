@@ -31,6 +31,7 @@
 #include "wk_common.h"
 #include "wk_kernels.h"
 #include "wk_mfma_layout.h"
+#include "wk_tail.h"
 
 namespace wk {
 
@@ -1034,6 +1035,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
 #endif
     if (i < NV) out.put(i, acc);
   }
+  if (ga.tail.on) grad_tail<64 * 2 * PAIRS>(ga.tail, ga.partial, (int)gridDim.x, (float4*)lds);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1399,6 +1401,7 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
   }
   GP_MARK(9);  // slab
   GP_FLUSH();
+  if (ga.tail.on) grad_tail<256 * TEAMS>(ga.tail, ga.partial, (int)gridDim.x, (float4*)lds);
 }
 
 // the weight image from the flat parameters (initialisation, wk_set_weights)
