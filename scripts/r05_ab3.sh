@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 L=$GRAFT_REPO_ROOT/ppo-bipedalwalker_amd
 OUT=gpurun_out/ab3; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_grad_scale.py tests/test_gpu_baseline_shapes.py tests/test_gpu_multirank.py tests/test_gpu_api2.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/tests.log 2>&1; rc=$?; tail -3 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
-for rep in 1 2; do for lib in libwk_nopool.so libwk.so libwk_pool3.so; do
+for rep in 1 2; do for lib in libwk_nopool.so libwk.so libwk_pool3.so libwk_pool1.so libwk_pool2.so; do
   echo "== $lib" >> $OUT/ab.log
   WK_LIB=$L/$lib REPS=5 timeout -k 10 300 python -u scripts/regime_ab.py 65536,8192 >> $OUT/ab.log 2>&1 || exit $?
 done; done
