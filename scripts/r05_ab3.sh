@@ -18,3 +18,4 @@ for rep in 1 2; do for t in 0 1; do
   WK_GRAD_TAIL=$t timeout -k 10 300 python -u scripts/update_ab.py 10 >> $OUT/upd.log 2>&1 || exit $?
 done; done
 grep -v amdgpu.ids $OUT/upd.log
+bash scripts/r05_region_pool.sh
