@@ -37,7 +37,8 @@ enum ProfKind { PK_PHYS = 0, PK_GRAD, PK_REDUCE, PK_ADAM, PK_ALLRED, PK_RET, PK_
 struct wk_ctx {
   wk_config cfg;
   int grad_impl = -1;  // matrix-core gradient kernel (wk::GI_*; -1 = by minibatch size)
-  bool grad_tail = true;  // single-GPU minibatch tail fused into the gradient kernel (WK_GRAD_TAIL)
+  int grad_tail = 0;  // single-GPU minibatch tail fused into the gradient kernel (WK_GRAD_TAIL: 0 off,
+                     // 1 release / acquire hand-off, 2 sc1 hand-off; off by default, measured slower)
   uint32_t* tail_cnt = nullptr;  // device: [0] block-arrival counter, [1] bounded-wait error
   uint32_t tail_seq = 0;         // the counter's value after the last fused launch
   bool tail_used = false;        // a fused launch ran since the last error check
@@ -314,7 +315,7 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   // per device; wk_create is the only place, so launches never race on it)
   if (wk::configure_device_kernels() != hipSuccess) { x->err = "hipFuncSetAttribute failed"; return fail(WK_ERR_HIP); }
   x->grad_impl = wk::grad_impl_env();
-  if (const char* e = getenv("WK_GRAD_TAIL")) x->grad_tail = atoi(e) != 0;
+  if (const char* e = getenv("WK_GRAD_TAIL")) x->grad_tail = atoi(e);
   if (hipDeviceGetAttribute(&x->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     x->n_cu = 0;  // (no fused tail then)
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1075,12 +1076,12 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   // one GPU, Adam, a matrix-core kernel with a tail (ws / tp / tp1), every block resident at
   // once (at most one per CU): the ordered reduction + Adam run in the gradient launch's last
   // blocks (wk_tail.h grad_tail) -- the same association, one launch per minibatch
-  const bool fused = apply_adam && !multi && wpb == 0 && gi != wk::GI_MF && c->grad_tail &&
+  const bool fused = apply_adam && !multi && wpb == 0 && gi != wk::GI_MF && c->grad_tail > 0 &&
                      nblocks <= 256 && nblocks <= c->n_cu;  // (RG x RG slabs: one-launch form)
   if (fused) {
     c->tail_used = true;
     c->tail_seq += (uint32_t)nblocks;
-    g.tail.on = 1;
+    g.tail.on = c->grad_tail;
     g.tail.cnt = c->tail_cnt;
     g.tail.err = c->tail_cnt + 1;
     g.tail.target = c->tail_seq;

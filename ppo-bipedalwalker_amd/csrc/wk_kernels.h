@@ -86,7 +86,7 @@ struct AdamArgs {
 struct GradTail {
   uint32_t* cnt;     // the context's monotone block-arrival counter (device)
   uint32_t target;   // its value once every block of this launch has arrived
-  int on;            // 0: no tail (the separate reduction launch follows)
+  int on;            // 0: no tail (the separate reduction launch follows); 1 release / acquire, 2 sc1 hand-off
   float* grad;       // the summed slab
   uint32_t* err;     // set if a tail block's bounded wait ran out
   AdamArgs a;

@@ -37,7 +37,16 @@ __device__ __forceinline__ void adam_apply(const AdamArgs& a, int p, float gr, f
 // One job of the one-launch reduction for nblocks <= RG * RG (thread t of 256: group gi = t / QB,
 // quad qi = t % QB; gs: the job's [RG][QB] float4 LDS tile).  The caller's block meets the one
 // barrier inside whether or not it has a job (job < 0: barrier only).  ADAM: also Adam (a.W set).
-template <bool ADAM>
+// SC1: the slab loads are sc1 buffer loads (the fused tail's hand-off without an acquire fence:
+// MI355X_MICROARCH.md, inter-workgroup visibility, "valid forms": sc1 stores drained before the
+// counter, sc1 loads after it)
+__device__ __forceinline__ float4 slab_load_sc1(const float* slab, int q) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)slab, 0, SLAB * 4, 0x00020000);
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, q * 16, 0, 16);
+  return __builtin_bit_cast(float4, v);
+}
+template <bool ADAM, bool SC1 = false>
 __device__ __forceinline__ void reduce_job(int job, int t, const float* __restrict__ partial,
                                            int nblocks, float* grad, const AdamArgs& a, float4* gs) {
   const int qi = t % QB, gi = t / QB;
@@ -56,8 +65,10 @@ __device__ __forceinline__ void reduce_job(int job, int t, const float* __restri
     float4 v[RG];
 #pragma unroll
     for (int j = 0; j < RG; j++)
-      v[j] = (b0 + j < nblocks) ? ((const float4*)(partial + (size_t)(b0 + j) * SLAB))[q]
-                                : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      v[j] = (b0 + j < nblocks)
+                 ? (SC1 ? slab_load_sc1(partial + (size_t)(b0 + j) * SLAB, q)
+                        : ((const float4*)(partial + (size_t)(b0 + j) * SLAB))[q])
+                 : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
     for (int j = 0; j < RG; j++)
       if (b0 + j < nblocks) {
@@ -82,23 +93,30 @@ __device__ __forceinline__ void reduce_job(int job, int t, const float* __restri
 }
 
 // The fused minibatch tail of a gradient kernel (round 5): called by every
-// thread of every block after the block's slab stores.  Each block drains its stores, bumps the
-// launch's arrival counter (agent-scope release); the LAST min(nblocks, JOBS / jobs-per-block)
-// blocks to arrive become the tail: they wait (bounded) until every block of the launch has
-// arrived, acquire, and run the reduction jobs -- the same association as k_grad_reduce_fused, so
-// the same bits -- with Adam.  No grid barrier: only the last arrivers wait, and only for blocks
-// already running (the launch is at most one block per CU).  NT: threads per block (multiple of
-// 256); gs: >= NT / 256 * RG * QB float4 of LDS the block no longer needs.
+// thread of every block after the block's slab stores.  Each block drains its stores and bumps the
+// launch's arrival counter; the LAST min(nblocks, JOBS / jobs-per-block) blocks to arrive become
+// the tail: they wait (bounded) until every block of the launch has arrived and run the reduction
+// jobs -- the same association as k_grad_reduce_fused, so the same bits -- with Adam.  No grid
+// barrier: only the last arrivers wait, and only for blocks already running (the launch is at most
+// one block per CU).  Hand-off (T.on): 1 -- agent-scope release on the counter, acquire after the
+// wait; 2 -- the slabs' sc1 (write-through) stores drained before a relaxed counter, relaxed polls,
+// sc1 loads of the slabs (no fences).  NT: threads per block (multiple of 256); gs: >= NT / 256 *
+// RG * QB float4 of LDS the block no longer needs.
 template <int NT>
 __device__ __forceinline__ void grad_tail(const GradTail& T, const float* __restrict__ partial,
                                           int nblocks, float4* gs) {
   static_assert(NT % 256 == 0, "256-thread jobs");
   constexpr int JPB = NT / 256;
   __shared__ int s_rank;
+  const bool sc1 = T.on == 2;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores have left
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t t = __hip_atomic_fetch_add(T.cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    if (!sc1) {  // (MI355X_MICROARCH.md, valid forms: release, then a wait the compiler cannot drop)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const uint32_t t = __hip_atomic_fetch_add(T.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     s_rank = (int)(t - (T.target - (uint32_t)nblocks));  // 1 .. nblocks: this block's arrival
   }
   __syncthreads();
@@ -109,7 +127,7 @@ __device__ __forceinline__ void grad_tail(const GradTail& T, const float* __rest
   if (threadIdx.x == 0) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     int ok = 1;
-    while ((int)(__hip_atomic_load(T.cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - T.target) < 0) {
+    while ((int)(__hip_atomic_load(T.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - T.target) < 0) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s: never in a sound launch
         atomicOr(T.err, 1u);
         ok = 0;
@@ -117,7 +135,10 @@ __device__ __forceinline__ void grad_tail(const GradTail& T, const float* __rest
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (!sc1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
+    }
     s_ok = ok;
   }
   __syncthreads();
@@ -125,7 +146,8 @@ __device__ __forceinline__ void grad_tail(const GradTail& T, const float* __rest
   const int grp = threadIdx.x >> 8;
   for (int j0 = ti * JPB; j0 < TAIL_JOBS; j0 += ntail * JPB) {  // (block-uniform trip count)
     const int job = j0 + grp < TAIL_JOBS ? j0 + grp : -1;
-    reduce_job<true>(job, threadIdx.x & 255, partial, nblocks, T.grad, T.a, gs + grp * RG * QB);
+    if (sc1) reduce_job<true, true>(job, threadIdx.x & 255, partial, nblocks, T.grad, T.a, gs + grp * RG * QB);
+    else reduce_job<true, false>(job, threadIdx.x & 255, partial, nblocks, T.grad, T.a, gs + grp * RG * QB);
     __syncthreads();  // the job tile is free for the next round
   }
 }
