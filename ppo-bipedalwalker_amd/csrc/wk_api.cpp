@@ -1076,9 +1076,10 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   // one GPU, Adam, a matrix-core kernel with a tail (ws / tp / tp1), every block resident at
   // once (at most one per CU): the ordered reduction + Adam run in the gradient launch's last
   // blocks (wk_tail.h grad_tail) -- the same association, one launch per minibatch
-  const bool fused = apply_adam && !multi && wpb == 0 && gi != wk::GI_MF && c->grad_tail > 0 &&
-                     nblocks <= 256 && nblocks <= c->n_cu;  // (RG x RG slabs: one-launch form)
-  if (fused) {
+  const bool tail = apply_adam && !multi && wpb == 0 && gi != wk::GI_MF && c->grad_tail > 0 &&
+                    nblocks <= 256 && nblocks <= c->n_cu;  // (RG x RG slabs: one-launch form)
+  const bool fused = tail && c->grad_tail <= 2;  // (3 / 4: cost probes of the tail's counter / wait)
+  if (tail) {
     c->tail_used = true;
     c->tail_seq += (uint32_t)nblocks;
     g.tail.on = c->grad_tail;

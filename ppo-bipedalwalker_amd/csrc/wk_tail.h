@@ -108,7 +108,8 @@ __device__ __forceinline__ void grad_tail(const GradTail& T, const float* __rest
   static_assert(NT % 256 == 0, "256-thread jobs");
   constexpr int JPB = NT / 256;
   __shared__ int s_rank;
-  const bool sc1 = T.on == 2;
+  const bool sc1 = T.on == 2 || T.on == 4;  // (3 / 4: probes -- the counter / counter + wait only,
+                                            // the host still launches the separate reduction)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores have left
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -120,6 +121,7 @@ __device__ __forceinline__ void grad_tail(const GradTail& T, const float* __rest
     s_rank = (int)(t - (T.target - (uint32_t)nblocks));  // 1 .. nblocks: this block's arrival
   }
   __syncthreads();
+  if (T.on == 3) return;
   const int ntail = nblocks < (TAIL_JOBS + JPB - 1) / JPB ? nblocks : (TAIL_JOBS + JPB - 1) / JPB;
   const int ti = s_rank - 1 - (nblocks - ntail);
   if (ti < 0) return;  // (block-uniform) an early arriver: done
@@ -142,7 +144,7 @@ __device__ __forceinline__ void grad_tail(const GradTail& T, const float* __rest
     s_ok = ok;
   }
   __syncthreads();
-  if (!s_ok) return;
+  if (!s_ok || T.on == 4) return;
   const int grp = threadIdx.x >> 8;
   for (int j0 = ti * JPB; j0 < TAIL_JOBS; j0 += ntail * JPB) {  // (block-uniform trip count)
     const int job = j0 + grp < TAIL_JOBS ? j0 + grp : -1;
