@@ -76,3 +76,18 @@ def test_detail_file_round_trip(tmp_path):
     p = tmp_path / "sub" / "detail.json"
     rel = bench.write_detail(full, str(p))
     assert rel is not None and json.load(open(p)) == full
+
+
+def test_valu_ceiling_uses_the_launched_grid():
+    """the split kernels launch whole 4-wave blocks; the one-wave ceiling is priced on
+    the launched waves, not only on the waves that hold walkers"""
+    full = {"lanes_per_walker": 4, "walkers_per_wave": 8, "waves": 1024, "waves_launched": 1024}
+    c, why = bench.valu_ceiling_of(full)
+    assert c == bench.PEAK_NOFMA_ONE_WAVE and "1024 of 1024" in why
+    ragged = {"lanes_per_walker": 4, "walkers_per_wave": 2, "waves": 750, "waves_launched": 752}
+    c, why = bench.valu_ceiling_of(ragged)
+    assert abs(c - bench.PEAK_NOFMA_ONE_WAVE * 752 / 1024) < 1e-9 and "752 of 1024" in why
+    two = {"lanes_per_walker": 2, "walkers_per_wave": 32, "waves": 2048, "waves_launched": 2048}
+    assert bench.valu_ceiling_of(two)[0] == bench.PEAK_NOFMA
+    old = {"lanes_per_walker": 2, "walkers_per_wave": 32, "waves": 2048}  # a pre-round-5 mapping
+    assert bench.valu_ceiling_of(old)[0] == bench.PEAK_NOFMA
