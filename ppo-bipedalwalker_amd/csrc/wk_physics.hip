@@ -346,10 +346,7 @@ DEV bool sat_floor_split(const Poly<6>& A, const Poly<4>& F, float mnx, float mn
 // H = 2: the quad mapping (sub = this lane's half): SAT axes and contact faces split over
 // the leg's two lanes (leg-leg and leg-floor pairs of Poly<6> segments).
 // FS > 0: the contact faces through this lane's LDS column frec (stride FS, the pair mapping)
-// PRE: the caller has already found the bounding boxes overlapping (the rough floor's segment
-// loop, with the segment's box in closed form): the pair starts at the overlap's consequences.
-template <int NA, int NB, bool BSTATIC, bool TRACE, int L, bool GENERIC = false, int H = 1, int FS = 0,
-          bool PRE = false>
+template <int NA, int NB, bool BSTATIC, bool TRACE, int L, bool GENERIC = false, int H = 1, int FS = 0>
 DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB, const Mat& mB,
                       bool& colA, PairTraceDev* tr, int pi, int sub, RegionProf* rp = nullptr,
                       uint32_t* ec = nullptr, float4* frec = nullptr) {
@@ -359,12 +356,10 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   static_assert(!GENERIC || BSTATIC, "generic static floor polygon");
   constexpr bool FLAT = BSTATIC && !GENERIC;
   constexpr int EVK = !BSTATIC ? 0 : (NA == 5 ? 2 : 1);  // leg-leg, leg-floor, torso-floor
-  static_assert(!PRE || !FLAT, "the flat floor's SAT reuses A's box");
-  float mnx = 0.0f, mny = 0.0f, mxx = 0.0f, mxy = 0.0f;  // A's bounding box (sat_floor reuses it)
-  bool ov = true;
-  if constexpr (!PRE) aabb(A, mnx, mny, mxx, mxy);
-  if constexpr (PRE) {
-  } else if constexpr (FLAT) {
+  float mnx, mny, mxx, mxy;  // A's bounding box (the floor pass of sat_floor reuses it)
+  aabb(A, mnx, mny, mxx, mxy);
+  bool ov;
+  if constexpr (FLAT) {
     ov = mnx < 1050.0f && mxx > -50.0f && mny < 1050.0f && mxy > 900.0f;  // floor box
   } else {
     float b0x, b0y, b1x, b1y;
@@ -519,24 +514,11 @@ DEV void floor_pairs(Poly<N>& P, Dyn& D, const Mat& m, bool& col, PairTraceDev* 
   zero_dyn(dfl);
   const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};  // Metal, static: inverse mass/inertia 0
   if constexpr (ROUGH) {
-    // P's box once, and again only after a segment it overlapped (whose pair may have moved P);
-    // each segment's box in closed form -- vertices (x, 1050), (x - 120 | x for k = 0, yprev),
-    // (x, y), (x + 120, 1050) with integer heights in [800, 900) -- the same values aabb() takes
-    // over its vertices; the polygon is built only for an overlap.  Same candidates, same order,
-    // same arithmetic for every pair that resolves (RigidBody.cs:66-96): bit-identical.
-    float mnx, mny, mxx, mxy;
-    aabb(P, mnx, mny, mxx, mxy);
 #pragma unroll 1
     for (int k = 0; k < 10; k++) {
-      const float yp = ter[k * TS], y = ter[(k + 1) * TS];
-      const float x = -50.0f + 120.0f * (float)k;
-      const float b0x = k == 0 ? x : x - 120.0f, b1x = x + 120.0f;
-      const float b0y = __builtin_fminf(yp, y), b1y = 1050.0f;
-      if (!(mnx < b1x && mxx > b0x && mny < b1y && mxy > b0y)) continue;
       Poly<4> seg;
-      rough_segment(seg, k, yp, y);
-      resolve_pair<N, 4, true, TRACE, L, true, 1, 0, true>(P, D, m, seg, dfl, mf, col, tr, -1, sub, nullptr, ec);
-      aabb(P, mnx, mny, mxx, mxy);
+      rough_segment(seg, k, ter[k * TS], ter[(k + 1) * TS]);
+      resolve_pair<N, 4, true, TRACE, L, true>(P, D, m, seg, dfl, mf, col, tr, -1, sub, nullptr, ec);
     }
   } else {
     Poly<4> fl;
