@@ -1437,15 +1437,32 @@ typedef float pf4 __attribute__((ext_vector_type(4)));
 #ifndef WK_OPAQUE
 #define WK_OPAQUE 1
 #endif
+#ifndef WK_OPQ_LOOP
+#define WK_OPQ_LOOP 1
+#endif
 DEV uint32_t lane_opaque(uint32_t v) {
 #if WK_OPAQUE
   asm volatile("" : "+v"(v));
 #endif
   return v;
 }
+#ifndef WK_TRAJ_NT
+// the trajectory rows as plain stores (1: non-temporal).  Written bytes per rollout launch at
+// 65,536 walkers (rollouts only, profiles/r05_write_probe.txt): non-temporal 439 MiB, plain 403
+// MiB against 384 MiB algorithmic (385 MiB with the identity lane order): a walker the lane order
+// moved into another wave writes into lines that wave fills, and plain stores let the L2 merge
+// those parts before the line is written back; the one-byte done rows likewise (their 32 bytes
+// per wave share a 128-byte line with three other waves).  Time unchanged.
+#define WK_TRAJ_NT 0
+#endif
+template <typename T>
+DEV void st_row(T v, T* p) {
+  if (WK_TRAJ_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 DEV void st_nt4(float* p, float a, float b, float c, float d) {
   const pf4 v = {a, b, c, d};
-  __builtin_nontemporal_store(v, (pf4*)p);
+  st_row(v, (pf4*)p);
 }
 DEV pf4 pmfma(float a, float b, pf4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 DEV float plrelu(float z) { return z < 0.0f ? 0.2f * z : z; }  // == Math.Max(0.2 z, z), see mf_lrelu
@@ -1453,10 +1470,10 @@ DEV float plrelu(float z) { return z < 0.0f ? 0.2f * z : z; }  // == Math.Max(0.
 // Q = 2 (quad mapping): 16 walkers per wave, one N tile
 template <int Q>
 DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool writer,
-                     float* __restrict__ pl, float z3[4], float& value) {
+                     float* __restrict__ pl, float z3[4], float& value, int tx) {
   using namespace mf;
   constexpr int NT = 2 / Q;  // 16-walker tiles per wave
-  const int lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4, wl = lane >> (Q == 2 ? 2 : 1);
+  const int lane = tx & 63, n = lane & 15, g = lane >> 4, wl = lane >> (Q == 2 ? 2 : 1);
   float* tile = pl;          // [32 walkers][16]: 12 observations
   float* outs = pl + 512;    // [32 walkers][8]: z3[0..3], critic output (disjoint from tile)
   if (writer) {
@@ -1598,10 +1615,8 @@ void k_env_side(EnvParams P, StepArgs A) {
   // rough floor's terrain as well, which would leave one block per CU)
   constexpr int FS = !POOL && (((Q == 1 && !ROUGH) || (Q == 2 && WK_FACE_LDS_QUAD)) && WK_FACE_LDS) ? SIDE_BLOCK : 0;
   __shared__ float4 face_lds[FS ? 6 * SIDE_BLOCK : 1];
-  float4* const frec = face_lds + (FS ? threadIdx.x : 0);
   // the legs' stash across the policy section: the face column, or the pool region's first part
   constexpr int SS = POOL ? SIDE_BLOCK : FS;
-  float4* const stash = POOL ? pool_lds + (pool::STASH + threadIdx.x) : frec;
   PoolCtx pc{pool_lds, pool_cnt, 0u, true, true};
   if constexpr (POOL) {
     if (threadIdx.x < 2) pool_cnt[threadIdx.x] = 0;  // (read after the stages' first barrier)
@@ -1618,7 +1633,6 @@ void k_env_side(EnvParams P, StepArgs A) {
       ((pf4*)wz_lds)[i] = ((const pf4*)A.Wz)[i];
     __syncthreads();
   }
-  float* const wave_pol = (POOL ? (float*)(pool_lds + pool::POL) : pol_lds) + (POLICY ? (threadIdx.x >> 6) * 768 : 0);
   SideState s;
   load_side(s, A.st, e, side);
   const float dx = A.dxoff[e];
@@ -1646,6 +1660,17 @@ void k_env_side(EnvParams P, StepArgs A) {
   for (int k = 0; k < A.k_steps; k++) {
     float a[4], lp[4], obs[12];
     rp_mark(rp, RP_OTHER);
+    // every LDS address of the env-step derived from the thread index afresh (an opaque copy
+    // made inside the loop): hoisted out of the loop they were ten loop-invariant VGPRs that
+    // the register allocator kept in scratch (WK_OPQ_LOOP=0: the hoisted form)
+#if WK_OPQ_LOOP
+    const int tx = (int)lane_opaque(threadIdx.x);
+#else
+    const int tx = threadIdx.x;
+#endif
+    float4* const frec = face_lds + (FS ? tx : 0);
+    float4* const stash = POOL ? pool_lds + (pool::STASH + tx) : frec;
+    float* const wave_pol = (POOL ? (float*)(pool_lds + pool::POL) : pol_lds) + (POLICY ? (tx >> 6) * 768 : 0);
     if constexpr (POOL) {
       // which floor slots the block's walkers take this env-step (the list order changes only
       // at a reset); also the barrier that keeps the policy's stash / tiles from the last
@@ -1665,22 +1690,30 @@ void k_env_side(EnvParams P, StepArgs A) {
         asm volatile("" ::: "memory");
       }
       float z3[4], mean[4], v;
-      policy_mfma<Q>(wz_lds, obs, side == 0 && half == 0, wave_pol, z3, v);
+      policy_mfma<Q>(wz_lds, obs, side == 0 && half == 0, wave_pol, z3, v, tx);
 #pragma unroll
       for (int d = 0; d < 4; d++) mean[d] = tanhf(z3[d]);
-      sample_actions(P, A.lp_const, gid, t, mean, a, lp);
-      if (RECORD && leader) {  // streamed rows: 16-byte non-temporal stores keep the L2 for Wz
+      // (the walker's Philox counter word through an opaque copy: the first round's per-lane
+      // products are recomputed per env-step rather than hoisted into seven spilled VGPRs)
+      sample_actions(P, A.lp_const, WK_OPQ_LOOP ? (uint32_t)P.env_offset + lane_opaque((uint32_t)e) : gid, t, mean, a, lp);
+#ifndef WK_PROBE_SKIP
+#define WK_PROBE_SKIP 0  // traffic probe builds only: 1 skips the s rows, 2 the done bytes, 4 a / lp / v / r
+#endif
+      if (RECORD && leader) {  // the rows: 16-byte stores (st_row: plain, see WK_TRAJ_NT)
         // row base (uniform, SGPRs) + the lane's 32-bit offset (global_store saddr form): no
         // per-lane 64-bit pointer per array stays live across the env-step loop (they spilled)
         const size_t row = (size_t)(A.t0 + k) * n;
         const uint32_t eo = lane_opaque((uint32_t)e);
 #pragma unroll
         for (int q = 0; q < 3; q++)
-          st_nt4(A.traj_s + row * 12 + (eo * 12u + 4u * q), obs[4 * q], obs[4 * q + 1], obs[4 * q + 2],
-                 obs[4 * q + 3]);
-        st_nt4(A.traj_a + row * 4 + eo * 4u, a[0], a[1], a[2], a[3]);
-        st_nt4(A.traj_lp + row * 4 + eo * 4u, lp[0], lp[1], lp[2], lp[3]);
-        __builtin_nontemporal_store(v, A.traj_v + row + eo);
+          if (!(WK_PROBE_SKIP & 1))
+            st_nt4(A.traj_s + row * 12 + (eo * 12u + 4u * q), obs[4 * q], obs[4 * q + 1], obs[4 * q + 2],
+                   obs[4 * q + 3]);
+        if (!(WK_PROBE_SKIP & 4)) {
+          st_nt4(A.traj_a + row * 4 + eo * 4u, a[0], a[1], a[2], a[3]);
+          st_nt4(A.traj_lp + row * 4 + eo * 4u, lp[0], lp[1], lp[2], lp[3]);
+          st_row(v, A.traj_v + row + eo);
+        }
       }
       if constexpr (SS != 0 && WK_POLICY_STASH) {
         asm volatile("" ::: "memory");
@@ -1736,7 +1769,10 @@ void k_env_side(EnvParams P, StepArgs A) {
     }
     if (terminal) {
       int ep = s.episodes + 1;
-      make_template_side(s, dx);
+      // (dx through an opaque copy: the template's vertices computed here, not hoisted)
+      // (the start offset re-read here: a loop-invariant dx or the template's vertices from it
+      // would otherwise stay live, i.e. in scratch, across the whole loop)
+      make_template_side(s, WK_OPQ_LOOP ? A.dxoff[lane_opaque((uint32_t)e)] : dx);
       s.post = true;
       s.episodes = ep;
     }
@@ -1752,13 +1788,14 @@ void k_env_side(EnvParams P, StepArgs A) {
       if (A.done_out) A.done_out[krow + eo] = terminal ? 1 : 0;
       if (RECORD) {
         const size_t row = (size_t)(A.t0 + k) * n;
-        __builtin_nontemporal_store(reward, A.traj_r + row + eo);
-        __builtin_nontemporal_store((uint8_t)(terminal ? 1 : 0), A.traj_d + row + eo);
+        if (!(WK_PROBE_SKIP & 4)) st_row(reward, A.traj_r + row + eo);
+        if (!(WK_PROBE_SKIP & 2)) st_row((uint8_t)(terminal ? 1 : 0), A.traj_d + row + eo);
       }
     }
     t++;
   }
-  if (active && half == 0) store_side(s, A.st, lane_opaque((uint32_t)e), side);
+  // (the side and its record offsets formed here again: kept from the loads they stayed in scratch)
+  if (active && half == 0) store_side(s, A.st, lane_opaque((uint32_t)e), (int)(lane_opaque(threadIdx.x) & 1u));
 #ifdef WK_REGION_PROF
   if ((threadIdx.x & 63) == 0)
     for (int r = 0; r < RP_N; r++) {
@@ -1769,8 +1806,9 @@ void k_env_side(EnvParams P, StepArgs A) {
 #endif
   fault |= (uint32_t)pswap((float)fault);
   if (leader) {
-    A.rng_t[e] = t;
-    if (A.fault_out) A.fault_out[e] |= fault;
+    const uint32_t eo = lane_opaque((uint32_t)e);  // (addresses formed here, not kept from the loads)
+    A.rng_t[eo] = t;
+    if (A.fault_out) A.fault_out[eo] |= fault;
   }
 }
 
