@@ -645,10 +645,14 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
     const int pos = c * 16 + n;
     uint32_t idx = ga.base + (uint32_t)(pos < ga.samples ? pos : 0);
     if (ga.use_perm) idx = perm_apply(idx, ga.pk);
+    // (the lane group through an opaque copy: hoisted, `states + 4 g` was a per-lane 64-bit base
+    // the allocator kept in scratch and reloaded before every chunk's gather)
+    uint32_t go = (uint32_t)g;
+    asm volatile("" : "+v"(go));
     m.sv = f4{1.0f, 0.0f, 0.0f, 0.0f};  // lane group 3: the bias column
-    if (g < 3) m.sv = *(const f4*)(ga.states + (size_t)idx * 12 + 4 * g);
-    m.act = ga.actions[(size_t)idx * 4 + g];
-    m.lpo = ga.logp_old[(size_t)idx * 4 + g];
+    if (g < 3) m.sv = *(const f4*)(ga.states + ((size_t)idx * 12 + 4 * go));
+    m.act = ga.actions[(size_t)idx * 4 + go];
+    m.lpo = ga.logp_old[(size_t)idx * 4 + go];
     m.ret = ga.returns[idx];
     m.adv = ga.adv[idx];
     return m;
