@@ -909,26 +909,32 @@ struct SideState {
   bool post, terminal;
 };
 
-// the legs' 24 vertex coordinates to / from a lane's float4 column (stride FS); see k_env_side
-template <int FS>
+// the legs' 24 vertex coordinates (NR = 6 records; NR = 4: the first 16 of them) to / from a
+// lane's float4 column (stride FS); see k_env_side
+template <int FS, int NR = 6>
 DEV void park_legs(const SideState& s, float4* r) {
   r[0 * FS] = make_float4(s.lo.x[0], s.lo.x[1], s.lo.x[2], s.lo.x[3]);
   r[1 * FS] = make_float4(s.lo.x[4], s.lo.x[5], s.lo.y[0], s.lo.y[1]);
   r[2 * FS] = make_float4(s.lo.y[2], s.lo.y[3], s.lo.y[4], s.lo.y[5]);
   r[3 * FS] = make_float4(s.up.x[0], s.up.x[1], s.up.x[2], s.up.x[3]);
-  r[4 * FS] = make_float4(s.up.x[4], s.up.x[5], s.up.y[0], s.up.y[1]);
-  r[5 * FS] = make_float4(s.up.y[2], s.up.y[3], s.up.y[4], s.up.y[5]);
+  if constexpr (NR == 6) {
+    r[4 * FS] = make_float4(s.up.x[4], s.up.x[5], s.up.y[0], s.up.y[1]);
+    r[5 * FS] = make_float4(s.up.y[2], s.up.y[3], s.up.y[4], s.up.y[5]);
+  }
 }
-template <int FS>
+template <int FS, int NR = 6>
 DEV void unpark_legs(SideState& s, const float4* r) {
   float4 a = r[0 * FS], b = r[1 * FS], c = r[2 * FS];
   s.lo.x[0] = a.x; s.lo.x[1] = a.y; s.lo.x[2] = a.z; s.lo.x[3] = a.w;
   s.lo.x[4] = b.x; s.lo.x[5] = b.y; s.lo.y[0] = b.z; s.lo.y[1] = b.w;
   s.lo.y[2] = c.x; s.lo.y[3] = c.y; s.lo.y[4] = c.z; s.lo.y[5] = c.w;
-  a = r[3 * FS]; b = r[4 * FS]; c = r[5 * FS];
+  a = r[3 * FS];
   s.up.x[0] = a.x; s.up.x[1] = a.y; s.up.x[2] = a.z; s.up.x[3] = a.w;
-  s.up.x[4] = b.x; s.up.x[5] = b.y; s.up.y[0] = b.z; s.up.y[1] = b.w;
-  s.up.y[2] = c.x; s.up.y[3] = c.y; s.up.y[4] = c.z; s.up.y[5] = c.w;
+  if constexpr (NR == 6) {
+    b = r[4 * FS]; c = r[5 * FS];
+    s.up.x[4] = b.x; s.up.x[5] = b.y; s.up.y[0] = b.z; s.up.y[1] = b.w;
+    s.up.y[2] = c.x; s.up.y[3] = c.y; s.up.y[4] = c.z; s.up.y[5] = c.w;
+  }
 }
 
 template <int CTRL>
@@ -1615,6 +1621,14 @@ void k_env_side(EnvParams P, StepArgs A) {
   // rough floor's terrain as well, which would leave one block per CU)
   constexpr int FS = !POOL && (((Q == 1 && !ROUGH) || (Q == 2 && WK_FACE_LDS_QUAD)) && WK_FACE_LDS) ? SIDE_BLOCK : 0;
   __shared__ float4 face_lds[FS ? 6 * SIDE_BLOCK : 1];
+  // the rough floor's pair kernel has no face column (its terrain would push two blocks past the
+  // CU's LDS); a 4-record column (16 KB per block, 2 x 75 KB fit) parks 16 of the legs' 24
+  // vertex coordinates over the policy instead of leaving them to the spill
+#ifndef WK_ROUGH_STASH
+#define WK_ROUGH_STASH 1
+#endif
+  constexpr int RS = (!POOL && Q == 1 && ROUGH && WK_ROUGH_STASH) ? SIDE_BLOCK : 0;
+  __shared__ float4 rstash_lds[RS ? 4 * SIDE_BLOCK : 1];
   // the legs' stash across the policy section: the face column, or the pool region's first part
   constexpr int SS = POOL ? SIDE_BLOCK : FS;
   PoolCtx pc{pool_lds, pool_cnt, 0u, true, true};
@@ -1688,6 +1702,9 @@ void k_env_side(EnvParams P, StepArgs A) {
       if constexpr (SS != 0 && WK_POLICY_STASH) {
         park_legs<SS>(s, stash);
         asm volatile("" ::: "memory");
+      } else if constexpr (RS != 0) {
+        park_legs<RS, 4>(s, rstash_lds + tx);
+        asm volatile("" ::: "memory");
       }
       float z3[4], mean[4], v;
       policy_mfma<Q>(wz_lds, obs, side == 0 && half == 0, wave_pol, z3, v, tx);
@@ -1718,6 +1735,9 @@ void k_env_side(EnvParams P, StepArgs A) {
       if constexpr (SS != 0 && WK_POLICY_STASH) {
         asm volatile("" ::: "memory");
         unpark_legs<SS>(s, stash);
+      } else if constexpr (RS != 0) {
+        asm volatile("" ::: "memory");
+        unpark_legs<RS, 4>(s, rstash_lds + tx);
       }
       if constexpr (POOL) __syncthreads();  // stash and tiles read before the queues reuse them
     } else {
