@@ -68,3 +68,24 @@ def test_bench_ipc_fallback_when_one_rank_fails():
     assert out["config"]["exchange_checked"] is False
     assert "rank 1: IPC exchange test gave wrong sums" in p.stdout
     assert out["value"] > 0 and len(lines[0]) < 4096
+
+
+def test_bench_four_rank_ipc_rehearsal():
+    """four ranks on device 0 with the one-shot IPC exchange (three peers' gradients read per
+    minibatch, the flag protocol over four ranks): the shard split 4,096 / 4 = 1,024 walkers, the
+    exchange checked against the host all-reduce before timing, one JSON line"""
+    cmd = ["timeout", "-k", "10", "300", sys.executable, "-m", "torch.distributed.run",
+           "--nnodes=1", "--nproc-per-node", "4", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "4",
+           "--steps", "2", "--warmup", "1", "--rehearse", "--walkers-global", "4096",
+           "--horizon", "8", "--epochs", "1", "--regime-iters", "1", "--exchange", "ipc",
+           "--detail-file", ""]
+    p = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    assert p.returncode == 0, p.stdout[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 4 and out["config"]["walkers_per_gpu"] == 1024
+    assert out["config"]["exchange"] == "ipc" and out["config"]["exchange_checked"] is True
+    assert abs(out["value"] - 4096 * 8 * 2 / (out["ms_per_step"] * 2e-3)) < 1e-6 * out["value"]
+
