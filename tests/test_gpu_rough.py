@@ -112,3 +112,31 @@ def test_rough_first_segment_degenerate_edges(wk, orc, lanes):
             o, r, d = e.step(acts[t, i])
             assert r == rew[t, i] and d == done[t, i], (i, t)
     np.testing.assert_array_equal(eng.get_state(), np.stack([e.dump() for e in envs]))
+
+
+def test_rough_65536_rollout_sampled_replay(wk, orc):
+    """the rough floor's bench line at its size (`rough_floor_65536`: the pair mapping with the
+    fused policy, the lane order and the terrain in LDS over all 512 blocks): a sample of the
+    65,536 walkers -- the first and last of every eighth block and 256 at random -- replayed
+    through the oracle with the GPU's own recorded actions, states / rewards / dones and final
+    records bit for bit"""
+    n, T = 65536, 64
+    eng = wk.Engine(n, seed=SEED, Horizon=T, RandomizeStart=1, RoughFloor=1, Minibatch=n, Epochs=1)
+    assert eng.rollout_mapping()["lanes_per_walker"] == 2
+    eng.rollout(T)
+    tr = eng.get_trajectory(T)
+    state = eng.get_state()
+    blocks = np.arange(0, n // 128, 8)
+    rng = np.random.default_rng(65536)
+    sample = np.unique(np.concatenate([blocks * 128, blocks * 128 + 127, rng.choice(n, 256, replace=False)]))
+    ndone = 0
+    for i in sample:
+        e = orc.Env(dx=float(orc.env_offset(SEED, int(i))), rough=(SEED, int(i)))
+        for t in range(T):
+            np.testing.assert_array_equal(tr["states"][t, i], e.obs(), err_msg=f"env {i} t {t}")
+            _, r, d = e.step(tr["actions"][t, i])
+            assert r == tr["rewards"][t, i] and d == tr["dones"][t, i], (i, t)
+            ndone += d
+        np.testing.assert_array_equal(state[i], e.dump(), err_msg=f"env {i}")
+    assert ndone > 0
+    eng.close()
