@@ -114,21 +114,24 @@ def test_rough_first_segment_degenerate_edges(wk, orc, lanes):
     np.testing.assert_array_equal(eng.get_state(), np.stack([e.dump() for e in envs]))
 
 
-def test_rough_65536_rollout_sampled_replay(wk, orc):
-    """the rough floor's bench line at its size (`rough_floor_65536`: the pair mapping with the
-    fused policy, the lane order and the terrain in LDS over all 512 blocks): a sample of the
-    65,536 walkers -- the first and last of every eighth block and 256 at random -- replayed
-    through the oracle with the GPU's own recorded actions, states / rewards / dones and final
-    records bit for bit"""
-    n, T = 65536, 64
+@pytest.mark.parametrize("n,lanes", [(65536, 2), (8192, 4)], ids=["65536-pair", "8192-quad"])
+def test_rough_bench_size_rollout_sampled_replay(wk, orc, n, lanes):
+    """the rough floor's bench lines at their sizes (`rough_floor_65536`: the pair mapping,
+    `rough_floor_shard_8192`: the sparse quad mapping; the fused policy, the lane order and the
+    terrain in LDS over the whole grid): a sample of the walkers -- the first and last of every
+    eighth block and 256 at random -- replayed through the oracle with the GPU's own recorded
+    actions, states / rewards / dones and final records bit for bit"""
+    T = 64
     eng = wk.Engine(n, seed=SEED, Horizon=T, RandomizeStart=1, RoughFloor=1, Minibatch=n, Epochs=1)
-    assert eng.rollout_mapping()["lanes_per_walker"] == 2
+    m = eng.rollout_mapping()
+    assert m["lanes_per_walker"] == lanes
     eng.rollout(T)
     tr = eng.get_trajectory(T)
     state = eng.get_state()
-    blocks = np.arange(0, n // 128, 8)
-    rng = np.random.default_rng(65536)
-    sample = np.unique(np.concatenate([blocks * 128, blocks * 128 + 127, rng.choice(n, 256, replace=False)]))
+    wpb = 256 // lanes if lanes == 2 else 4 * m["walkers_per_wave"]  # walkers per 4-wave block
+    blocks = np.arange(0, n // wpb, 8)
+    rng = np.random.default_rng(n)
+    sample = np.unique(np.concatenate([blocks * wpb, blocks * wpb + wpb - 1, rng.choice(n, 256, replace=False)]))
     ndone = 0
     for i in sample:
         e = orc.Env(dx=float(orc.env_offset(SEED, int(i))), rough=(SEED, int(i)))
