@@ -275,6 +275,25 @@ static int validate(const wk_config* c, std::string& why) {
   return WK_OK;
 }
 
+// The rough floor's lane order (split mappings): the walkers sorted by start offset, so that a
+// wave's walkers stand over the same stretch of terrain and its floor-segment loop resolves the
+// union of fewer segments (Environment.cs:230-261: segments 240 px wide every 120 px; the
+// offsets span 200 px).  Static -- a walker keeps its offset, and rough-floor episodes end
+// within a few steps, so the flat floor's episode-0 partition has nothing to gather -- and
+// recomputed whenever the offsets change (wk_create, wk_set_offsets, wk_checkpoint_load).
+// Measured with the offsets themselves sorted by walker id (scripts/rough_dx_sort.py): rollout
+// 110 -> 87.6 ms at 65,536 walkers (pair), 63.9 -> 50.4 ms at 8,192 (quad).  Bit-identical:
+// every walker's arithmetic is keyed by its id (tests/test_gpu_order.py).
+static hipError_t rough_order_upload(wk_ctx* c, const float* dx_host) {
+  if (!c->order || !c->P.rough || !(c->P.lanes == 2 || c->P.lanes == 4)) return hipSuccess;
+  std::vector<int32_t> ord(c->n);
+  for (size_t e = 0; e < c->n; e++) ord[e] = (int32_t)e;
+  std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) {
+    return dx_host[a] < dx_host[b];  // (a NaN offset compares false: it keeps its relative place)
+  });
+  return hipMemcpy(c->order, ord.data(), sizeof(int32_t) * c->n, hipMemcpyHostToDevice);
+}
+
 int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx** out) {
   if (!out) { g_create_error = "out is NULL"; return WK_ERR_ARG; }
   *out = nullptr;
@@ -423,6 +442,10 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
     x->err = "initial upload failed";
     return fail(WK_ERR_HIP);
   }
+  if (rough_order_upload(x, dx.data()) != hipSuccess) {
+    x->err = "lane order upload failed";
+    return fail(WK_ERR_HIP);
+  }
   if (wk::launch_env_init(P, x->st, x->dxoff, nullptr, 0, x->stream) != hipSuccess ||
       wk::launch_xavier(x->W, seed, x->stream) != hipSuccess ||
       wk::launch_swizzle(x->W, x->Wz, x->stream) != hipSuccess ||
@@ -513,25 +536,28 @@ int wk_set_offsets(wk_ctx* c, const float* dx) {
   if (!c || !dx) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));  // queued kernels read dxoff on auto-reset
   HIPCHK(c, hipMemcpy(c->dxoff, dx, sizeof(float) * c->n, hipMemcpyHostToDevice));
+  HIPCHK(c, rough_order_upload(c, dx));
   return WK_OK;
 }
 
 // the env-step kernel of the context's mapping; with scene props the one-lane scene kernel.
-// The split mappings first order their lanes: episode-0 walkers in the last slots (wk_order.hip;
-// WK_ORDER=0 keeps the identity order, for measurements).  Not the quad mapping on the rough
-// floor: at one wave per SIMD the launch lasts as long as its slowest wave, and there the few
-// long-lived episode-0 walkers (rough-floor episodes end within a few steps) gathered into one
-// wave make it the slowest -- 63 -> 74 ms per rollout at 8,192 walkers (scripts/r04_rough2.sh);
-// on the flat floor the quad mapping gains 2-3 % and the pair mapping 9.5 %
+// The split mappings first order their lanes (WK_ORDER=0 keeps the identity order, for
+// measurements).  Flat floor: episode-0 walkers in the last slots (wk_order.hip, before every
+// launch; the quad mapping gains 2-3 %, the pair mapping 9.5 %).  Rough floor: the static order by
+// start offset (rough_order_upload) -- not the episode-0 partition, which at one wave per SIMD
+// gathered the few long-lived episode-0 walkers into one slowest wave (63 -> 74 ms per rollout
+// at 8,192 walkers, scripts/r04_rough2.sh)
 static hipError_t launch_physics(wk_ctx* c, int mode, wk::StepArgs& A) {
   if (c->scene.n_props > 0) {
     A.props = c->props;
     return wk::launch_env_scene(mode, c->P, A, c->scene, c->stream);
   }
-  if (c->order && (c->P.lanes == 2 || (c->P.lanes == 4 && !c->P.rough))) {
-    const hipError_t e = wk::launch_walker_order(c->st, c->n, c->order_cnt, c->order, c->order + c->n,
-                                                 c->stream);
-    if (e != hipSuccess) return e;
+  if (c->order && (c->P.lanes == 2 || c->P.lanes == 4)) {
+    if (!c->P.rough) {
+      const hipError_t e = wk::launch_walker_order(c->st, c->n, c->order_cnt, c->order, c->order + c->n,
+                                                   c->stream);
+      if (e != hipSuccess) return e;
+    }
     A.order = c->order;
   }
   return wk::launch_env_step(mode, c->P, A, c->stream);
@@ -1966,7 +1992,13 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
   HIPCHK(c, hipMemcpy(c->v, q, sizeof(float) * wk::NPARAM, hipMemcpyHostToDevice)); q += sizeof(float) * wk::NPARAM;
   HIPCHK(c, hipMemcpy(c->st, q, sizeof(float) * n * wk::NSTATE, hipMemcpyHostToDevice)); q += sizeof(float) * n * wk::NSTATE;
   HIPCHK(c, hipMemcpy(c->rng_t, q, sizeof(uint32_t) * n, hipMemcpyHostToDevice)); q += sizeof(uint32_t) * n;
-  HIPCHK(c, hipMemcpy(c->dxoff, q, sizeof(float) * n, hipMemcpyHostToDevice)); q += sizeof(float) * n;
+  HIPCHK(c, hipMemcpy(c->dxoff, q, sizeof(float) * n, hipMemcpyHostToDevice));
+  {
+    std::vector<float> dxh(n);
+    std::memcpy(dxh.data(), q, sizeof(float) * n);
+    HIPCHK(c, rough_order_upload(c, dxh.data()));
+  }
+  q += sizeof(float) * n;
   HIPCHK(c, hipMemcpy(c->mat, q, sizeof(int32_t) * n, hipMemcpyHostToDevice)); q += sizeof(int32_t) * n;
   HIPCHK(c, hipMemcpy(c->ep_acc, q, sizeof(double) * n, hipMemcpyHostToDevice)); q += sizeof(double) * n;
   HIPCHK(c, hipMemcpy(c->ep_len, q, sizeof(int32_t) * n, hipMemcpyHostToDevice)); q += sizeof(int32_t) * n;

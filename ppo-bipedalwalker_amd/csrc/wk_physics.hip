@@ -1713,6 +1713,9 @@ void k_env_side(EnvParams P, StepArgs A) {
       // (the walker's Philox counter word through an opaque copy: the first round's per-lane
       // products are recomputed per env-step rather than hoisted into seven spilled VGPRs)
       sample_actions(P, A.lp_const, WK_OPQ_LOOP ? (uint32_t)P.env_offset + lane_opaque((uint32_t)e) : gid, t, mean, a, lp);
+#ifndef WK_PROBE_SLOTROWS
+#define WK_PROBE_SLOTROWS 0  // probe builds only: trajectory rows at the lane slot, not the walker id
+#endif
 #ifndef WK_PROBE_SKIP
 #define WK_PROBE_SKIP 0  // traffic probe builds only: 1 skips the s rows, 2 the done bytes, 4 a / lp / v / r
 #endif
@@ -1720,7 +1723,7 @@ void k_env_side(EnvParams P, StepArgs A) {
         // row base (uniform, SGPRs) + the lane's 32-bit offset (global_store saddr form): no
         // per-lane 64-bit pointer per array stays live across the env-step loop (they spilled)
         const size_t row = (size_t)(A.t0 + k) * n;
-        const uint32_t eo = lane_opaque((uint32_t)e);
+        const uint32_t eo = lane_opaque((uint32_t)(WK_PROBE_SLOTROWS ? slot : e));
 #pragma unroll
         for (int q = 0; q < 3; q++)
           if (!(WK_PROBE_SKIP & 1))
@@ -1782,7 +1785,7 @@ void k_env_side(EnvParams P, StepArgs A) {
     }
     if (!side_finite(s)) fault |= 1u;
     const size_t krow = (size_t)k * n;  // (uniform) + the lane's 32-bit offset, as above
-    const uint32_t eo = lane_opaque((uint32_t)e);
+    const uint32_t eo = lane_opaque((uint32_t)(WK_PROBE_SLOTROWS ? slot : e));
     if (A.pos_out && leader) {
       A.pos_out[krow * 2 + eo * 2u] = s.posx;
       A.pos_out[krow * 2 + (eo * 2u + 1u)] = s.posy;

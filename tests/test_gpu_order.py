@@ -2,7 +2,8 @@
 
 Before every launch the lane-pair / quad mappings order their lanes so that walkers still in
 their first episode come first (their floor pairs run in the other list order,
-RigidBody.cs:66-96 / Walker.cs:212-234).  The order only decides which walkers share a wave;
+RigidBody.cs:66-96 / Walker.cs:212-234); on the rough floor the order is static, the walkers
+sorted by start offset (wk_api.cpp rough_order_upload, recomputed when the offsets change).  The order only decides which walkers share a wave;
 every walker's arithmetic, Philox stream and trajectory rows are its own, so a context with the
 ordering and one with the identity order (WK_ORDER=0, read at wk_create) must produce the same
 trajectories, walker records and PPO updates bit for bit -- here with short episodes
@@ -31,7 +32,7 @@ def _engine(wk, n, ordered, **cfg):
 
 
 @pytest.mark.parametrize("n,lanes,rough", [(3000, 4, 0), (4096, 4, 0), (20011, 2, 0), (40000, 2, 0),
-                                           (20011, 2, 1)])
+                                           (20011, 2, 1), (3000, 4, 1)])
 def test_lane_order_is_invisible(wk, n, lanes, rough):
     """rough = 1: the rough-floor pair kernel fills its per-walker terrain column in
     LDS from the reordered walker id"""
@@ -60,3 +61,40 @@ def test_lane_order_is_invisible(wk, n, lanes, rough):
     assert mixed  # launches started with both kinds of walker
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("lanes", [2, 4])
+def test_rough_offset_order_follows_the_offsets(wk, tmp_path, lanes):
+    """the rough floor's offset order is rebuilt when the offsets change: new offsets through
+    wk_set_offsets (reversed: the old order would now be the worst one) and a checkpoint written
+    by another context, loaded into both -- ordered and identity contexts stay bit-identical"""
+    n, T = 5000, 16
+    cfg = dict(Horizon=T, Minibatch=n * T // 4, Epochs=1, RandomizeStart=1, MaxTimesteps=30,
+               LanesPerWalker=lanes, RoughFloor=1)
+    a, b = _engine(wk, n, True, **cfg), _engine(wk, n, False, **cfg)
+    dx = np.linspace(199.0, 0.0, n).astype(np.float32)
+    for e in (a, b):
+        e.set_offsets(dx)
+        e.reset()
+        e.rollout(T)
+    ta, tb = a.get_trajectory(T), b.get_trajectory(T)
+    for k in ta:
+        np.testing.assert_array_equal(ta[k], tb[k], err_msg=k)
+    other = wk.Engine(n, seed=SEED, **cfg)  # (a checkpoint must come from the same seed)
+    other.set_offsets(np.random.default_rng(3).permutation(dx))
+    other.reset()
+    for _ in range(2):
+        other.rollout(T)
+    path = str(tmp_path / "other.ckpt")
+    other.checkpoint_save(path)
+    other.close()
+    for e in (a, b):
+        e.checkpoint_load(path)
+        e.rollout(T)
+    ta, tb = a.get_trajectory(T), b.get_trajectory(T)
+    for k in ta:
+        np.testing.assert_array_equal(ta[k], tb[k], err_msg=f"after load: {k}")
+    np.testing.assert_array_equal(a.get_state(), b.get_state())
+    a.close()
+    b.close()
+
