@@ -514,11 +514,28 @@ DEV void floor_pairs(Poly<N>& P, Dyn& D, const Mat& m, bool& col, PairTraceDev* 
   zero_dyn(dfl);
   const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};  // Metal, static: inverse mass/inertia 0
   if constexpr (ROUGH) {
+    // Only the segments whose x-extent can reach the part's are visited: segment k spans
+    // [x_k - 120, x_k + 120] (k = 0: from x_0), x_k = -50 + 120 k, so a segment with
+    // x_k + 120 <= mnx or x_k - 120 >= mxx fails the pair's own bounding-box test; the range
+    // below keeps one more segment on each side (rounding of the bound itself), so every
+    // segment it leaves out is more than 100 px clear.  In list order as before; once the
+    // part has moved (a resolved pair) the remaining segments are all visited, as the full
+    // loop would test them against the moved part.  A non-finite or huge box: every segment.
+    // With the lane order by start offset a part spans 3-5 segments of the 10.
+    float mnx, mny, mxx, mxy;
+    aabb(P, mnx, mny, mxx, mxy);
+    int k = 0, kend = 9;
+    if (mnx >= -1.0e6f && mxx <= 1.0e6f) {
+      k = max(0, (int)floorf((mnx - 70.0f) * (1.0f / 120.0f)) - 1);
+      kend = min(9, (int)floorf((mxx + 170.0f) * (1.0f / 120.0f)) + 1);
+    }
 #pragma unroll 1
-    for (int k = 0; k < 10; k++) {
+    for (; k <= kend; k++) {
       Poly<4> seg;
       rough_segment(seg, k, ter[k * TS], ter[(k + 1) * TS]);
+      const float cx0 = P.cx, cy0 = P.cy;
       resolve_pair<N, 4, true, TRACE, L, true>(P, D, m, seg, dfl, mf, col, tr, -1, sub, nullptr, ec);
+      if (!(P.cx == cx0 && P.cy == cy0)) kend = 9;
     }
   } else {
     Poly<4> fl;
