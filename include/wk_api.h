@@ -239,6 +239,8 @@ int wk_num_envs(const wk_ctx* ctx);
 /* environment */
 int wk_reset(wk_ctx* ctx, const uint8_t* mask /* n_env or NULL = all */);
 int wk_set_materials(wk_ctx* ctx, const int32_t* mat_id /* n_env */);
+/* start offsets (applied at each walker's next reset); on the rough floor the split mappings'
+   lane order (walkers sorted by offset, results unaffected) is rebuilt from them */
 int wk_set_offsets(wk_ctx* ctx, const float* dx /* n_env; start x = 125 + dx */);
 int wk_step(wk_ctx* ctx, const float* actions_or_null /* k*n_env*4, unclipped */, int k_steps,
             float* obs /* k*n_env*12 or NULL */, float* reward /* k*n_env or NULL */,
