@@ -1483,7 +1483,7 @@ DEV void st_row(T v, T* p) {
   if (WK_TRAJ_NT) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
-DEV void st_nt4(float* p, float a, float b, float c, float d) {
+DEV void st_row4(float* p, float a, float b, float c, float d) {
   const pf4 v = {a, b, c, d};
   st_row(v, (pf4*)p);
 }
@@ -1744,11 +1744,11 @@ void k_env_side(EnvParams P, StepArgs A) {
 #pragma unroll
         for (int q = 0; q < 3; q++)
           if (!(WK_PROBE_SKIP & 1))
-            st_nt4(A.traj_s + row * 12 + (eo * 12u + 4u * q), obs[4 * q], obs[4 * q + 1], obs[4 * q + 2],
+            st_row4(A.traj_s + row * 12 + (eo * 12u + 4u * q), obs[4 * q], obs[4 * q + 1], obs[4 * q + 2],
                    obs[4 * q + 3]);
         if (!(WK_PROBE_SKIP & 4)) {
-          st_nt4(A.traj_a + row * 4 + eo * 4u, a[0], a[1], a[2], a[3]);
-          st_nt4(A.traj_lp + row * 4 + eo * 4u, lp[0], lp[1], lp[2], lp[3]);
+          st_row4(A.traj_a + row * 4 + eo * 4u, a[0], a[1], a[2], a[3]);
+          st_row4(A.traj_lp + row * 4 + eo * 4u, lp[0], lp[1], lp[2], lp[3]);
           st_row(v, A.traj_v + row + eo);
         }
       }
@@ -1809,7 +1809,6 @@ void k_env_side(EnvParams P, StepArgs A) {
     }
     if (terminal) {
       int ep = s.episodes + 1;
-      // (dx through an opaque copy: the template's vertices computed here, not hoisted)
       // (the start offset re-read here: a loop-invariant dx or the template's vertices from it
       // would otherwise stay live, i.e. in scratch, across the whole loop)
       make_template_side(s, WK_OPQ_LOOP ? A.dxoff[lane_opaque((uint32_t)e)] : dx);
