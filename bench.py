@@ -102,6 +102,10 @@ def parse():
                         "checked bit for bit against a rank-order reference before timing, and "
                         "RCCL on every rank if the mapping, the test round or the check fails), "
                         "or the RCCL all-reduce")
+    p.add_argument("--xch-profile", action="store_true",
+                   help="N > 1 with the IPC exchange: after timing, one untimed iteration with the "
+                        "exchange kernel's per-block clock stamps (wk_comm_xch_profile): wait for "
+                        "peers versus own work per minibatch, in the detail file and the line")
     p.add_argument("--detail-file", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
                    help="full result (every roofline field, event rates, notes); the stdout line "
                         "is the compact <= 4 KB summary and names this file ('' = do not write)")
@@ -487,15 +491,26 @@ def compact_line(full, detail_file=None):
         out["configs"] = sm
     if "rehearsal" in full:
         out["rehearsal"] = full["rehearsal"]
+    if full.get("xch_profile"):
+        out["xch_profile_us"] = [None if r is None else
+                                 {k: _r(r[k + "_us_median"], 3) for k in ("span", "wait", "own", "gap")}
+                                 for r in full["xch_profile"]["per_rank"]]
     if detail_file:
         out["detail_file"] = detail_file
     line = json.dumps(out, separators=(",", ":"))
     if len(line) >= LINE_LIMIT:  # never lose the headline: drop the optional parts first
-        for k in ("configs", "regime", "rollout_env_steps_per_s"):
+        for k in ("configs", "xch_profile_us", "regime", "rollout_env_steps_per_s", "cpu_baseline",
+                  "roofline_update", "config"):
             out.pop(k, None)
             line = json.dumps(out, separators=(",", ":"))
             if len(line) < LINE_LIMIT:
                 break
+    if len(line) >= LINE_LIMIT:  #  the contract keys alone + where the rest went
+        out = {k: out[k] for k in keys + ("detail_file",) if k in out}
+        for k in ("metric", "data"):
+            if isinstance(out.get(k), str):
+                out[k] = out[k][:400]
+        line = json.dumps(out, separators=(",", ":"))
     return line
 
 
@@ -628,6 +643,28 @@ def ipc_exchange_setup(wk, eng, mk_engine, rank, world, horizon, dist, torch, np
     return int(same and identical), check
 
 
+def xch_stamp_summary(st):
+    """per-minibatch split of the IPC exchange kernel (k_reduce_xch_adam) from its per-block
+    constant-clock stamps [launch, block, (entry, published, peers seen, exit)], 10 ns ticks:
+    span = last exit - first entry of the launch; wait = a block's (peers seen - published);
+    own = (published - entry) + (exit - peers seen), the block's reduction, publish, peer reads and
+    Adam; gap = next launch's first entry - this launch's last exit (the gradient kernel between)"""
+    import numpy as np
+    if len(st) == 0:
+        return None
+    st = st.astype(np.float64) * 0.01  # ticks of the 100 MHz clock -> microseconds
+    span = st[:, :, 3].max(axis=1) - st[:, :, 0].min(axis=1)
+    wait = st[:, :, 2] - st[:, :, 1]
+    own = (st[:, :, 1] - st[:, :, 0]) + (st[:, :, 3] - st[:, :, 2])
+    gap = st[1:, :, 0].min(axis=1) - st[:-1, :, 3].max(axis=1)
+    med = lambda a: float(np.median(a)) if a.size else None
+    return {"launches": int(st.shape[0]), "blocks": int(st.shape[1]),
+            "span_us_median": med(span), "span_us_mean": float(span.mean()),
+            "wait_us_median": med(np.median(wait, axis=1)), "wait_us_max_median": med(wait.max(axis=1)),
+            "own_us_median": med(np.median(own, axis=1)), "own_us_max_median": med(own.max(axis=1)),
+            "gap_us_median": med(gap)}
+
+
 def main():
     args = parse()
     json_out = _claim_stdout()
@@ -722,6 +759,16 @@ def main():
     # level-2 in-update mean for the update roofline)
     grad_burst_ms = eng.time_gradient(shard.minibatch_local, GRAD_BURST)
     grad_burst_ev_ms = eng.time_gradient(shard.minibatch_local, GRAD_BURST, per_launch_events=True)
+    # untimed: one iteration with the exchange kernel's per-block clock stamps
+    xch_prof = None
+    if args.xch_profile and exchange == "ipc":
+        n_mb = args.epochs * (shard.n_local * T // shard.minibatch_local)
+        eng.xch_profile(n_mb)
+        time_iterations(eng, args, 1, T, upd, barrier)
+        mine = xch_stamp_summary(eng.xch_stamps(n_mb))
+        eng.xch_profile(0)
+        xch_prof = [None] * world
+        dist.all_gather_object(xch_prof, mine)
     # untimed: the timed iteration's episode count, then its physics events (counting replay of
     # its actions from the restored state) for the rollout roofline
     eng.restore()
@@ -786,6 +833,8 @@ def main():
     }
     if xch_check is not None:
         out["config"]["exchange_check"] = xch_check
+    if xch_prof is not None:
+        out["xch_profile"] = {"per_rank": xch_prof, "note": xch_stamp_summary.__doc__.split(";")[0]}
     if world == 1 and not args.rehearse:
         out["allreduce_1rank"] = allreduce_one_rank(wk, eng, args, T, upd)
     if rank == 0 and world == 1 and not args.no_extras:
@@ -796,6 +845,9 @@ def main():
         ex["config4_shard_8192"] = extra_config(wk, torch, args, 8192, 8192, 65536, T)
         ex["config5_shard_8192"] = extra_config(wk, torch, args, 8192, 8192, 65536, T,
                                                 materials=True)
+        #  config 5 at its stated size: 65,536 walkers with per-env materials
+        ex["config5_materials_65536"] = extra_config(wk, torch, args, 65536, 65536, 65536, T,
+                                                     materials=True)
         ex["rough_floor_65536"] = extra_config(wk, torch, args, 65536, 65536, 65536, T, rough=True)
         ex["rough_floor_shard_8192"] = extra_config(wk, torch, args, 8192, 8192, 65536, T,
                                                     rough=True)

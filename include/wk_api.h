@@ -265,7 +265,34 @@ int wk_step_device(wk_ctx* ctx, const float* d_actions_or_null, int k_steps, flo
 int wk_step_traced(wk_ctx* ctx, const float* actions /* n_env*4 */, wk_pair_trace* trace);
 int wk_get_obs(wk_ctx* ctx, float* obs /* n_env*12 */);
 int wk_get_state(wk_ctx* ctx, float* state /* n_env*WK_STATE_FLOATS */);
+/* wk_set_state (and wk_checkpoint_load's walker records) refuse, with WK_ERR_ARG and the walker
+ * and body in wk_last_error, a state whose leg segments are not rigid walker poles: the kernels
+ * project a pole onto its own edge axes over fixed vertex groups (exact for Pole.FromSize's
+ * shape, Pole.cs:18-34, moved and rotated rigidly), so every vertex must stay >= 3.5 px outside
+ * the groups it is left out of (the template has 7.5 px).  Non-finite poles are not checked.
+ * wk_check_state runs the same check on host memory (no context, no device): WK_OK, or
+ * WK_ERR_ARG with the first failing walker and body (record body index) in *bad_env / *bad_body. */
 int wk_set_state(wk_ctx* ctx, const float* state /* n_env*WK_STATE_FLOATS */);
+int wk_check_state(const float* state, int n_env, int* bad_env, int* bad_body);
+/* The reference's per-body call shape (new entry points for a host that keeps
+ * Environment.StepObjects, Environment.cs:126-143): per substep it calls Joint.Step on the 4 joints
+ * (Joint.cs:31-41) and IObject.Update (Objects/IObject.cs:9) on every body of its list, after
+ * Walker.TakeActions (Walker.cs:66-75).  The GPU resolves a whole env-step (every substep, joint
+ * and body of every walker of the context) in one launch, so:
+ *   wk_take_actions   stores walker env's 4 torques (unclipped; clipped in-kernel) for the next
+ *                     frame; a walker given none keeps its current torques (no kick)
+ *   wk_object_update  the frame's FIRST call runs one env-step of every walker with those torques
+ *                     (returns 1); the other list_count * Iterations - 1 calls of the frame are
+ *                     counted and return 0 (deltaTime: the caller's substep; the context's
+ *                     DeltaTime is used)
+ *   wk_joint_step     resolved inside the step: a no-op (returns 0)
+ *   wk_body_order     walker env's body list now: part ids (0 LLL, 1 LLU, 2 Body, 3 RLL, 4 RLU,
+ *                     5 floor / 5..14 rough-floor segments) floor last in episode 0 and first after
+ *                     a reset (Walker.cs:191-234) -- at most 15 */
+int wk_take_actions(wk_ctx* ctx, int env, const float* actions /* 4 */);
+int wk_object_update(wk_ctx* ctx, int list_count, float delta_time);
+int wk_joint_step(wk_ctx* ctx);
+int wk_body_order(wk_ctx* ctx, int env, int* parts /* 15 */, int* count);
 int wk_get_body_view(wk_ctx* ctx, int env, int body /* 0..4 walker, 5 floor (5..14 rough-floor segments) */,
                      wk_body_view* out);
 
@@ -413,6 +440,14 @@ int wk_comm_set_timeout(wk_ctx* ctx, double seconds);
 /* the context's minibatch exchange: *kind 0 none, 1 RCCL, 2 host callback, 3 IPC; *flags bit 0:
  * the IPC exchange region is uncached device memory (else coarse-grained hipMalloc memory) */
 int wk_comm_info(wk_ctx* ctx, int* kind, int* flags);
+/* IPC exchange timing (new; the exchange replaces the all-reduce before PPOAgent.cs:344-345's
+ * Optimise): with minibatches > 0 every exchange launch of the context stamps the GPU's 100 MHz
+ * constant clock per block at four points -- entry, its slab published (flag released), every
+ * peer's flag seen, exit (peer slabs read, Adam stored) -- into a device ring of `minibatches`
+ * launches; 0 frees the ring.  wk_comm_xch_stamps copies the last min(stamped, max_launches)
+ * launches, oldest first, as stamps[(launch * blocks + block) * 4 + point] (ticks of 10 ns). */
+int wk_comm_xch_profile(wk_ctx* ctx, int minibatches);
+int wk_comm_xch_stamps(wk_ctx* ctx, uint64_t* stamps, int max_launches, int* launches, int* blocks);
 
 /* profiling */
 /* level 0 off; 1: HIP events around each rollout / returns pass / whole PPO update (cheap

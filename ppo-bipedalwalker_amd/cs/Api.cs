@@ -4,9 +4,12 @@
 // Bodies/RigidBody.cs (the read side a renderer and GetState use), Walker/Walker.cs:49-223.
 // The C++ mirror of the same surface is csrc/host/nea.hpp; this file follows it member for
 // member.  The physics state lives on the GPU (one context per environment), so a RigidBody
-// here is a view of one body of one walker (wk_get_body_view) and IObject.Update steps the
-// walker's whole list once, as Environment.StepObjects does (Environment.cs:126-143).  Errors
-// are logged and the operation skipped (ErrorLogger.LogError, the reference's convention).
+// here is a view of one body of one walker (wk_get_body_view).  A host that keeps the reference's
+// Environment.StepObjects loop (Environment.cs:126-143: per substep Joint.Step on the 4 joints,
+// then IObject.Update on every body of the list) calls wk_object_update list.Count * Iterations
+// times per frame: the frame's first call runs the env-step of every walker with the torques
+// Walker.TakeActions stored (wk_take_actions), the others are counted no-ops.  Errors are logged
+// and the operation skipped (ErrorLogger.LogError, the reference's convention).
 using System;
 using System.Collections.Generic;
 
@@ -49,9 +52,9 @@ namespace NEA.Bodies
 
     // Bodies/RigidBody.cs, the read side (GetVertices / GetCentroid / GetLinearVelocity /
     // GetAngularVelocity / GetAngle / Collided / IsStatic) of body `Part` (0 LLL, 1 LLU, 2 Body,
-    // 3 RLL, 4 RLU, 5 Floor: the episode-0 list order, Walker.cs:197) of walker `Env`.
-    // Update (IObject) steps the walker's whole list once: the GPU resolves every body of the
-    // list in the reference's order inside one env-step, so stepping one body alone does not exist.
+    // 3 RLL, 4 RLU, 5 Floor -- 5..14 the rough floor's segments) of walker `Env`.
+    // Update (IObject): the GPU resolves every body of the list in the reference's order inside
+    // one env-step, so stepping one body alone does not exist; the frame is assembled natively.
     public sealed class RigidBody : IObject
     {
         readonly IntPtr _ctx;
@@ -78,38 +81,24 @@ namespace NEA.Bodies
         public bool Collided => View().Collided != 0;
         public bool IsStatic => View().IsStatic != 0;
 
-        // IObject.Update (Objects/IObject.cs:9): one Environment.StepObjects of the context's
-        // walkers (Environment.cs:126-143) with the torques Walker.TakeActions set since the last
-        // step (the policy samples the walkers none were given for; wk_step clips in-kernel)
+        // IObject.Update (Objects/IObject.cs:9), called list.Count * Iterations times per frame by
+        // Environment.StepObjects (Environment.cs:130-141): the frame's first call steps every
+        // walker of the context once with the torques Walker.TakeActions stored (a walker given
+        // none keeps its torques: no kick), the frame's other calls are no-ops (wk_object_update)
         public void Update(List<RigidBody> rigidBodies, float deltaTime)
         {
-            var a = PendingActions.Take(_ctx);
-            Wk.Ok(_ctx, Wk.wk_step(_ctx, a, 1, null, null, null, null), "Exception occurred during the environment update", Console.Error.WriteLine);
+            int r = Wk.wk_object_update(_ctx, rigidBodies.Count, deltaTime);
+            if (r < 0) Wk.Ok(_ctx, r, "Exception occurred during the environment update", Console.Error.WriteLine);
         }
     }
-}
 
-namespace NEA.Native
-{
-    // the torques Walker.TakeActions set for a context's next step (nea.hpp's pending_)
-    public static class PendingActions
+    // Joint.Step (Joint.cs:31-41): the joints of every walker are resolved inside the frame's
+    // env-step (wk_joint_step is a no-op kept for the call shape)
+    public sealed class Joint
     {
-        static readonly Dictionary<IntPtr, float[]> _pending = new();
-        public static void Set(IntPtr ctx, int walker, float[] actions)
-        {
-            if (!_pending.TryGetValue(ctx, out var all))
-            {
-                all = new float[Wk.wk_num_envs(ctx) * WkConst.Act];
-                _pending[ctx] = all;
-            }
-            Array.Copy(actions, 0, all, walker * WkConst.Act, WkConst.Act);
-        }
-        public static float[]? Take(IntPtr ctx)
-        {
-            if (!_pending.TryGetValue(ctx, out var all)) return null;
-            _pending.Remove(ctx);
-            return all;
-        }
+        readonly IntPtr _ctx;
+        internal Joint(IntPtr ctx) { _ctx = ctx; }
+        public void Step() => Wk.wk_joint_step(_ctx);
     }
 }
 
@@ -118,6 +107,7 @@ namespace NEA.Walker
     using NEA.Bodies;
     using NEA.Materials;
     using NEA.Native;
+    using NEA.Objects;
 
     // Walker/Walker.cs:49-223 for walker `Index` of a context (a Walker owns no state of its own:
     // its bodies, torques, Collided flags and episode counter live in the context's records)
@@ -145,16 +135,28 @@ namespace NEA.Walker
             rigidBodies.AddRange(Bodies());
         }
 
-        // the list RigidBody.ResolveCollisions walks: [LLL, LLU, Body, RLL, RLU, Floor]
+        // the list RigidBody.ResolveCollisions walks, in its current order (wk_body_order):
+        // [LLL, LLU, Body, RLL, RLU, Floor] in episode 0, [Floor, LLL, LLU, Body, RLL, RLU] after a
+        // reset (Reset removes the walker's bodies and CreateBodies appends them after the floor,
+        // Walker.cs:191-234); the rough floor's ten segments stand where the floor does
         public List<RigidBody> Bodies()
         {
-            var l = new List<RigidBody>(6);
-            for (int b = 0; b < 6; b++) l.Add(new RigidBody(_ctx, Index, b));
+            var parts = new int[15];
+            var l = new List<RigidBody>(15);
+            if (!Wk.Ok(_ctx, Wk.wk_body_order(_ctx, Index, parts, out int n), "Exception while reading the body list", _log))
+                return l;
+            for (int i = 0; i < n; i++) l.Add(new RigidBody(_ctx, Index, parts[i]));
             return l;
         }
 
+        // the part of this walker's list (by part id, whatever the list order)
+        RigidBody Part(int part) => new RigidBody(_ctx, Index, part);
+
+        // GetJoints (Walker.cs:102): [bodyJointLeft, bodyJointRight, leftJoint, rightJoint]
+        public List<Joint> GetJoints() => new List<Joint> { new(_ctx), new(_ctx), new(_ctx), new(_ctx) };
+
         // Walker.Update (:49-54): terminal once the body or an upper leg touched the floor
-        public bool Terminal => Bodies()[2].Collided || Bodies()[1].Collided || Bodies()[4].Collided;
+        public bool Terminal => Part(2).Collided || Part(1).Collided || Part(4).Collided;
 
         // GetActions (:57-62): the policy's sample for this walker's state
         public float[] GetActions(float[] state, out float[] logProbabilities)
@@ -168,12 +170,12 @@ namespace NEA.Walker
             return a;
         }
 
-        // TakeActions (:66-75): the torques of the next step; a wrong-sized action is ignored
+        // TakeActions (:66-75): the torques of the next frame; a wrong-sized action is ignored
         // like the reference's height check; the joints' SetTorque runs inside the step
         public void TakeActions(float[] actions)
         {
             if (actions.Length != WkConst.Act) return;
-            PendingActions.Set(_ctx, Index, actions);
+            Wk.Ok(_ctx, Wk.wk_take_actions(_ctx, Index, actions), "Exception while setting the torques", _log);
         }
 
         // GetState (:132-152)
@@ -188,7 +190,7 @@ namespace NEA.Walker
         }
 
         // GetPosition (:108-111): the torso's centroid
-        public (float X, float Y) GetPosition() => Bodies()[2].GetCentroid();
+        public (float X, float Y) GetPosition() => Part(2).GetCentroid();
 
         // Reset (:212-223): this walker back to its template (post-reset list order)
         public void Reset(List<RigidBody> rigidBodies)

@@ -159,6 +159,11 @@ public static class Wk
     [DllImport(Lib)] public static extern int wk_get_obs(IntPtr ctx, float[] obs);
     [DllImport(Lib)] public static extern int wk_get_state(IntPtr ctx, float[] state);
     [DllImport(Lib)] public static extern int wk_set_state(IntPtr ctx, float[] state);
+    [DllImport(Lib)] public static extern int wk_check_state(float[] state, int nEnv, out int badEnv, out int badBody);
+    [DllImport(Lib)] public static extern int wk_take_actions(IntPtr ctx, int env, float[] actions);
+    [DllImport(Lib)] public static extern int wk_object_update(IntPtr ctx, int listCount, float deltaTime);
+    [DllImport(Lib)] public static extern int wk_joint_step(IntPtr ctx);
+    [DllImport(Lib)] public static extern int wk_body_order(IntPtr ctx, int env, int[] parts, out int count);
     [DllImport(Lib)] public static extern int wk_get_body_view(IntPtr ctx, int env, int body, out WkBodyView view);
     [DllImport(Lib)] public static extern int wk_set_scene(IntPtr ctx, WkProp[]? props, int nProps);
     [DllImport(Lib)] public static extern int wk_get_prop_view(IntPtr ctx, int env, int prop, out WkPropView view);
@@ -209,6 +214,8 @@ public static class Wk
     [DllImport(Lib)] public static extern int wk_comm_init_ipc(IntPtr ctx, int rank, int nRanks, byte[] handles);
     [DllImport(Lib)] public static extern int wk_comm_info(IntPtr ctx, out int kind, out int flags);
     [DllImport(Lib)] public static extern int wk_comm_set_timeout(IntPtr ctx, double seconds);
+    [DllImport(Lib)] public static extern int wk_comm_xch_profile(IntPtr ctx, int minibatches);
+    [DllImport(Lib)] public static extern int wk_comm_xch_stamps(IntPtr ctx, ulong[] stamps, int maxLaunches, out int launches, out int blocks);
     [UnmanagedFunctionPointer(CallingConvention.Cdecl)] public delegate int HostAllReduce(IntPtr buf, int n, IntPtr user);
     [DllImport(Lib)] public static extern int wk_comm_init_host(IntPtr ctx, int rank, int nRanks, HostAllReduce fn, IntPtr user);
 

@@ -37,12 +37,6 @@ enum ProfKind { PK_PHYS = 0, PK_GRAD, PK_REDUCE, PK_ADAM, PK_ALLRED, PK_RET, PK_
 struct wk_ctx {
   wk_config cfg;
   int grad_impl = -1;  // matrix-core gradient kernel (wk::GI_*; -1 = by minibatch size)
-  int grad_tail = 0;  // single-GPU minibatch tail fused into the gradient kernel (WK_GRAD_TAIL: 0 off,
-                     // 1 release / acquire hand-off, 2 sc1 hand-off; off by default, measured slower)
-  uint32_t* tail_cnt = nullptr;  // device: [0] block-arrival counter, [1] bounded-wait error
-  uint32_t tail_seq = 0;         // the counter's value after the last fused launch
-  bool tail_used = false;        // a fused launch ran since the last error check
-  int n_cu = 0;                  // compute units of the device (the fused tail needs every block resident)
   int device = 0;
   int n = 0;
   uint64_t seed = 0;
@@ -106,6 +100,13 @@ struct wk_ctx {
   uint32_t* xch_err = nullptr;         // device word: a peer never published
   bool xch_uncached = false;           // the region is uncached device memory (else hipMalloc)
   uint64_t xch_timeout_ticks = 0;      // bounded peer wait (WK_XCH_TIMEOUT_S / wk_comm_set_timeout)
+  uint64_t* xch_stamps = nullptr;      // wk_comm_xch_profile: [cap][blocks][XCH_POINTS] clock ring
+  int xch_stamp_cap = 0;
+  int64_t xch_stamp_launches = 0;      // launches stamped since the ring was (re)armed
+  // the reference's per-body call shape (wk_take_actions / wk_object_update)
+  std::vector<float> pend;             // [n][4] torques wk_take_actions stored for the next frame
+  std::vector<uint8_t> pend_set;       // [n] walker given torques since the last frame
+  int64_t frame_calls = 0, frame_len = 0;
   // profiling
   int prof = 0;  // profile level
   struct Ev { int kind; hipEvent_t a, b; int64_t units; };
@@ -334,9 +335,6 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   // per device; wk_create is the only place, so launches never race on it)
   if (wk::configure_device_kernels() != hipSuccess) { x->err = "hipFuncSetAttribute failed"; return fail(WK_ERR_HIP); }
   x->grad_impl = wk::grad_impl_env();
-  if (const char* e = getenv("WK_GRAD_TAIL")) x->grad_tail = atoi(e);
-  if (hipDeviceGetAttribute(&x->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
-    x->n_cu = 0;  // (no fused tail then)
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) {
     x->err = "hipStreamCreate failed";
     return fail(WK_ERR_HIP);
@@ -364,16 +362,13 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   // the quad mapping with fewer walkers per wave (the other lanes replay them) while one wave
   // per SIMD still holds every walker (1,024 SIMDs): each wave's divergent branches are the
   // union over fewer walkers -- rollout 5.72 -> 5.52 ms per 16 env-steps at 8,192 walkers
-  // (eight per wave), physics only 5.95 -> 5.62.  WK_QUAD_SPARSE=0: always sixteen
+  // (eight per wave), physics only 5.95 -> 5.62.  Test hook (tests/test_gpu_parity.py, the
+  // sparse mapping against the dense one): WK_QUAD_SPARSE=0 at wk_create, always sixteen
   {
     const char* sp = getenv("WK_QUAD_SPARSE");
     int wpw = 16;
     if (!(sp && sp[0] == '0'))
       while (wpw > 1 && (size_t)n_env <= (size_t)512 * wpw) wpw >>= 1;  // n / (wpw / 2) <= 1,024 waves
-    if (const char* f = getenv("WK_QUAD_WPW")) {  // (experiments: a forced power of two)
-      const int v = atoi(f);
-      if (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) wpw = v;
-    }
     P.wpw = wpw;
   }
   const float PI_F = 3.14159265358979323846f;
@@ -394,7 +389,6 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   ALLOC(x->m, sizeof(float) * wk::NPARAM);
   ALLOC(x->v, sizeof(float) * wk::NPARAM);
   ALLOC(x->grad, sizeof(float) * wk::SLAB);
-  ALLOC(x->tail_cnt, 2 * sizeof(uint32_t));
   ALLOC(x->ts, sizeof(float) * 12 * n * T);
   ALLOC(x->ta, sizeof(float) * 4 * n * T);
   ALLOC(x->tlp, sizeof(float) * 4 * n * T);
@@ -412,7 +406,8 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
   ALLOC(x->ep_count, sizeof(uint64_t));
   ALLOC(x->ep_log, sizeof(wk::EpisodeRecDev) * x->ep_cap);
   ALLOC(x->loss_log, sizeof(float) * 2 * x->loss_cap);
-  if (P.lanes == 2 || P.lanes == 4) {  // (WK_ORDER=0: identity lane order, for measurements)
+  // test hook (tests/test_gpu_order.py, the lane order against the identity order): WK_ORDER=0
+  if (P.lanes == 2 || P.lanes == 4) {
     const char* o = getenv("WK_ORDER");
     if (!(o && o[0] == '0')) {
       ALLOC(x->order, sizeof(int32_t) * 3 * n);  // order, then the swap ranks' scratch
@@ -432,7 +427,6 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
       hipMemcpy(x->mat, mt.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(x->rng_t, 0, sizeof(uint32_t) * n) != hipSuccess ||
       hipMemset(x->m, 0, sizeof(float) * wk::NPARAM) != hipSuccess ||
-      hipMemset(x->tail_cnt, 0, 2 * sizeof(uint32_t)) != hipSuccess ||
       hipMemset(x->v, 0, sizeof(float) * wk::NPARAM) != hipSuccess ||
       hipMemset(x->td, 0, n * T) != hipSuccess ||
       hipMemset(x->ep_acc, 0, sizeof(double) * n) != hipSuccess ||
@@ -468,10 +462,11 @@ int wk_destroy(wk_ctx* c) {
     if (p) (void)hipIpcCloseMemHandle(p);
   if (c->xch) (void)hipFree(c->xch);
   if (c->xch_err) (void)hipFree(c->xch_err);
+  if (c->xch_stamps) (void)hipFree(c->xch_stamps);
   void* bufs[] = {c->st, c->dxoff, c->mat, c->rng_t, c->W, c->Wz, c->m, c->v, c->grad, c->ts, c->ta,
                   c->tlp, c->tr, c->tv, c->tret, c->tadv, c->td, c->partial, c->scratch, c->scratch2,
                   c->ep_acc, c->ep_len, c->ep_scratch, c->ep_rowcnt, c->ep_count, c->ep_log,
-                  c->loss_log, c->props, c->snap, c->counts, c->order, c->order_cnt, c->tail_cnt};
+                  c->loss_log, c->props, c->snap, c->counts, c->order, c->order_cnt};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -479,27 +474,11 @@ int wk_destroy(wk_ctx* c) {
   return WK_OK;
 }
 
-// the fused minibatch tail's bounded wait ran out (never in a sound launch: every block of the
-// launch is resident) -- reported at the next synchronising call
-static int tail_status(wk_ctx* c) {
-  if (!c->tail_used) return WK_OK;
-  uint32_t err = 0;
-  HIPCHK(c, hipMemcpyAsync(&err, c->tail_cnt + 1, sizeof err, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  c->tail_used = false;
-  if (err) {
-    SETERR(c, "fused minibatch tail: a tail block's wait for the gradient launch's blocks ran out "
-           "(some Adam steps incomplete)");
-    return WK_ERR_HIP;
-  }
-  return WK_OK;
-}
-
 int wk_sync(wk_ctx* c) {
   DevGuard dg_(c);
   if (!c) return WK_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  return tail_status(c);
+  return WK_OK;
 }
 
 int wk_num_envs(const wk_ctx* c) { return c ? c->n : 0; }
@@ -614,6 +593,71 @@ int wk_step(wk_ctx* c, const float* actions, int k, float* obs, float* reward, u
   return WK_OK;
 }
 
+// ---------------- the reference's per-body call shape ----------------
+// Environment.StepObjects (Environment.cs:126-143) calls, per substep, Joint.Step on the 4 joints
+// and IObject.Update (Objects/IObject.cs:9) on every body of the list: list_count * Iterations
+// Update calls per frame.  The GPU resolves the whole frame in one launch, so the frame's FIRST
+// Update call runs one env-step of every walker and the rest are counted no-ops; the torques are
+// the ones Walker.TakeActions (Walker.cs:66-75) stored since the last frame, and a walker given
+// none keeps its joints' current torques (Joint.SetTorque with the same value: no kick,
+// Joint.cs:56-61) -- as in the reference, where nothing else changes them.
+static int current_torques(wk_ctx* c, float* out /* [n][4] */) {
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy2D(out, sizeof(float) * 4, c->st + wk::S_TORQUE, sizeof(float) * wk::NSTATE,
+                        sizeof(float) * 4, c->n, hipMemcpyDeviceToHost));
+  return WK_OK;
+}
+
+int wk_take_actions(wk_ctx* c, int env, const float* actions) {
+  if (!c || !actions || env < 0 || env >= c->n) return WK_ERR_ARG;
+  if (c->pend_set.empty()) {
+    c->pend.assign((size_t)c->n * 4, 0.0f);
+    c->pend_set.assign((size_t)c->n, 0);
+  }
+  for (int j = 0; j < 4; j++) c->pend[(size_t)env * 4 + j] = actions[j];
+  c->pend_set[env] = 1;
+  return WK_OK;
+}
+
+int wk_object_update(wk_ctx* c, int list_count, float delta_time) {
+  DevGuard dg_(c);
+  if (!c || list_count <= 0 || !(delta_time >= 0.0f)) return WK_ERR_ARG;
+  int stepped = 0;
+  if (c->frame_calls == 0) {
+    c->frame_len = (int64_t)list_count * c->cfg.Iterations;
+    std::vector<float> a((size_t)c->n * 4);
+    if (int r = current_torques(c, a.data())) return r;  // (the state as of this frame)
+    for (size_t e = 0; e < c->pend_set.size(); e++)
+      if (c->pend_set[e])
+        for (int j = 0; j < 4; j++) a[e * 4 + j] = c->pend[e * 4 + j];
+    std::fill(c->pend_set.begin(), c->pend_set.end(), (uint8_t)0);
+    if (int r = wk_step(c, a.data(), 1, nullptr, nullptr, nullptr, nullptr)) return r;
+    stepped = 1;
+  }
+  if (++c->frame_calls >= c->frame_len) c->frame_calls = 0;
+  return stepped;
+}
+
+int wk_joint_step(wk_ctx* c) { return c ? WK_OK : WK_ERR_ARG; }
+
+int wk_body_order(wk_ctx* c, int env, int* parts, int* count) {
+  DevGuard dg_(c);
+  if (!c || !parts || !count || env < 0 || env >= c->n) return WK_ERR_ARG;
+  float post = 0.0f;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(&post, c->st + (size_t)env * wk::NSTATE + wk::S_POSTRESET, sizeof(float),
+                      hipMemcpyDeviceToHost));
+  const int nfloor = c->P.rough ? 10 : 1;  // the floor body ids are 5 .. 5 + nfloor - 1
+  int k = 0;
+  if (post != 0.0f)
+    for (int f = 0; f < nfloor; f++) parts[k++] = 5 + f;
+  for (int b = 0; b < 5; b++) parts[k++] = b;  // CreateBodies' order: LLL, LLU, Body, RLL, RLU
+  if (post == 0.0f)
+    for (int f = 0; f < nfloor; f++) parts[k++] = 5 + f;
+  *count = k;
+  return WK_OK;
+}
+
 int wk_step_sampled(wk_ctx* c, int k, float* states, float* actions, float* logp, float* values,
                     float* reward, uint8_t* done, float* next_obs, uint32_t* fault,
                     float* position) {
@@ -702,9 +746,76 @@ int wk_get_state(wk_ctx* c, float* state) {
   return WK_OK;
 }
 
+// the rigid-pole shortcut (pole_own_minmax, csrc/wk_device.h) projects a walker
+// pole onto its own edge axes with min / max over fixed vertex groups, which equals the reference's
+// min / max over all six vertices (SATCollision.cs:63-76 ProjectPoints) only while the pole keeps
+// its template shape (Pole.FromSize, Pole.cs:18-34): every vertex left out of a group lies >= 7.5
+// px beyond the group's extreme.  A state from outside (wk_set_state, wk_checkpoint_load) must keep
+// that margin; the kernel's own states do (rigid motion, << 1 px of rounding drift).
+// Required margin: POLE_MARGIN_PX, above the worst-case drift bound (~3 px over 50,000 substeps).
+// Poles with a non-finite coordinate are not checked (the NaN path is exact).
+static constexpr double POLE_MARGIN_PX = 3.5;
+static const int kPoleGroups[6][2][3] = {  // per own edge: {min group, max group}, -1 = unused
+    {{0, 1, 2}, {3, 4, 5}}, {{0, 1, 2}, {3, 4, 5}}, {{2, 3, -1}, {5, 0, -1}},
+    {{3, 4, 5}, {0, 1, 2}}, {{3, 4, 5}, {0, 1, 2}}, {{5, 0, -1}, {2, 3, -1}}};
+// the smallest margin of one pole (record floats x0 y0 .. x5 y5), or +inf if non-finite
+static double pole_margin(const float* v) {
+  for (int i = 0; i < 12; i++)
+    if (!std::isfinite(v[i])) return INFINITY;
+  double worst = INFINITY;
+  for (int e = 0; e < 6; e++) {
+    const int e1 = (e + 1) % 6;
+    const double ex = (double)v[2 * e1] - v[2 * e], ey = (double)v[2 * e1 + 1] - v[2 * e + 1];
+    const double len = std::sqrt(ex * ex + ey * ey);
+    if (!(len > 0.0)) return -INFINITY;  // a zero edge: not a rigid template pole
+    const double ax = -ey / len, ay = ex / len;
+    double p[6];
+    for (int i = 0; i < 6; i++) p[i] = ax * v[2 * i] + ay * v[2 * i + 1];
+    bool inmin[6] = {}, inmax[6] = {};
+    double gmin = INFINITY, gmax = -INFINITY;
+    for (int k = 0; k < 3; k++) {
+      const int a = kPoleGroups[e][0][k], b = kPoleGroups[e][1][k];
+      if (a >= 0) { inmin[a] = true; gmin = std::min(gmin, p[a]); }
+      if (b >= 0) { inmax[b] = true; gmax = std::max(gmax, p[b]); }
+    }
+    for (int i = 0; i < 6; i++) {
+      if (!inmin[i]) worst = std::min(worst, p[i] - gmin);
+      if (!inmax[i]) worst = std::min(worst, gmax - p[i]);
+    }
+  }
+  return worst;
+}
+
+int wk_check_state(const float* state, int n_env, int* bad_env, int* bad_body) {
+  if (!state || n_env <= 0) return WK_ERR_ARG;
+  static const int poles[4] = {wk::LLL, wk::LLU, wk::RLL, wk::RLU};
+  for (int e = 0; e < n_env; e++)
+    for (int b : poles)
+      if (!(pole_margin(state + (size_t)e * wk::NSTATE + (size_t)b * wk::BSTRIDE) >= POLE_MARGIN_PX)) {
+        if (bad_env) *bad_env = e;
+        if (bad_body) *bad_body = b;
+        return WK_ERR_ARG;
+      }
+  if (bad_env) *bad_env = -1;
+  if (bad_body) *bad_body = -1;
+  return WK_OK;
+}
+
+static int check_state_or_fail(wk_ctx* c, const float* state) {
+  int e = -1, b = -1;
+  if (wk_check_state(state, c->n, &e, &b) != WK_OK) {
+    SETERR(c, "walker %d body %d is not a rigid walker pole (a vertex group closer than %.1f px to "
+           "the excluded vertices on one of its own edge axes: deformed or reordered vertices); "
+           "the state is refused", e, b, POLE_MARGIN_PX);
+    return WK_ERR_ARG;
+  }
+  return WK_OK;
+}
+
 int wk_set_state(wk_ctx* c, const float* state) {
   DevGuard dg_(c);
   if (!c || !state) return WK_ERR_ARG;
+  if (int r = check_state_or_fail(c, state)) return r;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(c->st, state, sizeof(float) * wk::NSTATE * c->n, hipMemcpyHostToDevice));
   return WK_OK;
@@ -1064,6 +1175,13 @@ int wk_set_trajectory(wk_ctx* c, int horizon, const float* s, const float* a, co
   return WK_OK;
 }
 
+// the ring slot of the next stamped exchange launch (wk_comm_xch_profile), or null
+static uint64_t* xch_stamp_slot(wk_ctx* c) {
+  if (!c->xch_stamps) return nullptr;
+  const int64_t slot = c->xch_stamp_launches++ % c->xch_stamp_cap;
+  return c->xch_stamps + (size_t)slot * wk::xch_blocks() * wk::XCH_POINTS;
+}
+
 // one minibatch: gradient kernel -> ordered block reduction -> [RCCL all-reduce] -> Adam
 // wpb == 0: the matrix-core kernel (wk_ppo_mfma.hip); wpb >= 1: the lane-per-neuron
 // kernel (wk_ppo.hip; wpb == 1 visits the samples in minibatch order)
@@ -1099,22 +1217,6 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
   // with a communicator (any size, also one rank) the collective path runs: reduction,
   // RCCL all-reduce, Adam -- a single-GPU test then covers the multi-GPU sequence
   const bool multi = c->comm != nullptr || c->host_ar != nullptr || c->ipc;
-  // one GPU, Adam, a matrix-core kernel with a tail (ws / tp / tp1), every block resident at
-  // once (at most one per CU): the ordered reduction + Adam run in the gradient launch's last
-  // blocks (wk_tail.h grad_tail) -- the same association, one launch per minibatch
-  const bool tail = apply_adam && !multi && wpb == 0 && gi != wk::GI_MF && c->grad_tail > 0 &&
-                    nblocks <= 256 && nblocks <= c->n_cu;  // (RG x RG slabs: one-launch form)
-  const bool fused = tail && c->grad_tail <= 2;  // (3 / 4: cost probes of the tail's counter / wait)
-  if (tail) {
-    c->tail_used = true;
-    c->tail_seq += (uint32_t)nblocks;
-    g.tail.on = c->grad_tail;
-    g.tail.cnt = c->tail_cnt;
-    g.tail.err = c->tail_cnt + 1;
-    g.tail.target = c->tail_seq;
-    g.tail.grad = c->grad;
-    g.tail.a = a;
-  }
   {
     ProfScope ps(c, PK_GRAD, 0, 2);
     HIPCHK(c, wpb == 0 ? wk::launch_ppo_grad_mfma(g, nblocks, gi, c->stream)
@@ -1134,11 +1236,11 @@ static int minibatch(wk_ctx* c, wk::GradArgs g, int wpb, int apply_adam) {
     x.timeout_ticks = c->xch_timeout_ticks;
     x.t = (uint32_t)c->adam_t;
     x.a = a;
+    x.stamps = xch_stamp_slot(c);
     HIPCHK(c, wk::launch_reduce_xch_adam(x, c->stream));
     return WK_OK;
   }
   if (apply_adam && !multi) {  // one GPU: the last reduction stage applies Adam
-    if (fused) return WK_OK;     // (done by the gradient kernel's last blocks)
     ProfScope ps(c, PK_REDUCE, 0, 2);
     HIPCHK(c, wk::launch_grad_reduce_adam(c->partial, nblocks, part2, c->grad, a, c->stream));
     return WK_OK;
@@ -1343,7 +1445,6 @@ int wk_ppo_update(wk_ctx* c, const wk_ppo_args* args, float* critic_diag, float*
   float diag[3] = {0, 0, 0};
   HIPCHK(c, hipMemcpyAsync(diag, c->grad + wk::NPARAM, sizeof(diag), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (int r = tail_status(c)) return r;
   if (critic_diag) *critic_diag = diag[0];
   if (actor_diag) *actor_diag = diag[1];
   return WK_OK;
@@ -1571,6 +1672,42 @@ int wk_comm_info(wk_ctx* c, int* kind, int* flags) {
   if (!c || !kind || !flags) return WK_ERR_ARG;
   *kind = c->ipc ? 3 : c->host_ar ? 2 : c->comm ? 1 : 0;
   *flags = (c->xch && c->xch_uncached) ? 1 : 0;
+  return WK_OK;
+}
+
+int wk_comm_xch_profile(wk_ctx* c, int minibatches) {
+  DevGuard dg_(c);
+  if (!c || minibatches < 0 || minibatches > (1 << 20)) return WK_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // (no launch still writes the old ring)
+  if (c->xch_stamps) (void)hipFree(c->xch_stamps);
+  c->xch_stamps = nullptr;
+  c->xch_stamp_cap = 0;
+  c->xch_stamp_launches = 0;
+  if (minibatches == 0) return WK_OK;
+  const size_t bytes = sizeof(uint64_t) * (size_t)minibatches * wk::xch_blocks() * wk::XCH_POINTS;
+  HIPCHK(c, hipMalloc((void**)&c->xch_stamps, bytes));
+  HIPCHK(c, hipMemset(c->xch_stamps, 0, bytes));
+  c->xch_stamp_cap = minibatches;
+  return WK_OK;
+}
+
+int wk_comm_xch_stamps(wk_ctx* c, uint64_t* stamps, int max_launches, int* launches, int* blocks) {
+  DevGuard dg_(c);
+  if (!c || !launches || !blocks || max_launches < 0 || (max_launches > 0 && !stamps)) return WK_ERR_ARG;
+  *blocks = wk::xch_blocks();
+  if (!c->xch_stamps) { *launches = 0; return WK_OK; }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int64_t have = std::min<int64_t>(c->xch_stamp_launches, c->xch_stamp_cap);
+  const int n = (int)std::min<int64_t>(have, max_launches);
+  const size_t per = (size_t)wk::xch_blocks() * wk::XCH_POINTS;
+  // the last n launches, oldest first (the ring wraps at cap)
+  for (int i = 0; i < n; i++) {
+    const int64_t launch = c->xch_stamp_launches - n + i;
+    const int64_t slot = launch % c->xch_stamp_cap;
+    HIPCHK(c, hipMemcpy(stamps + (size_t)i * per, c->xch_stamps + (size_t)slot * per,
+                        sizeof(uint64_t) * per, hipMemcpyDeviceToHost));
+  }
+  *launches = n;
   return WK_OK;
 }
 
@@ -1981,6 +2118,12 @@ int wk_checkpoint_load(wk_ctx* c, const char* path) {
     SETERR(c, "checkpoint '%s' has scene props, which need the one-lane mapping "
               "(LanesPerWalker 0 or 1)", path);
     return WK_ERR_CONFIG;
+  }
+  {  // the walker records keep rigid template poles, checked before any write
+    std::vector<float> rec(n * wk::NSTATE);
+    memcpy(rec.data(), data.data() + sizeof h + ext_bytes + sizeof(float) * 3 * wk::NPARAM,
+           sizeof(float) * rec.size());
+    if (int r = check_state_or_fail(c, rec.data())) return r;
   }
   // the scene first: wk_set_scene is all-or-nothing and is the last step that can fail on
   // anything but a device error

@@ -9,12 +9,6 @@
 #include "wk_common.h"
 #include "wk_sincos_small.h"
 
-#ifndef WK_PACKED_ROT
-#define WK_PACKED_ROT 1
-#endif
-#ifndef WK_PACKED_PROJ
-#define WK_PACKED_PROJ 1
-#endif
 
 namespace wk {
 
@@ -135,7 +129,6 @@ DEV void floor_poly(Poly<4>& f) {
 // Skeleton.Move (Skeleton.cs:76-85)
 template <int N>
 DEV void move(Poly<N>& p, V2 d) {
-#if WK_PACKED_ROT
   const pf2 dx = {d.x, d.x}, dy = {d.y, d.y};
 #pragma unroll
   for (int i = 0; i + 1 < N; i += 2) {
@@ -143,10 +136,6 @@ DEV void move(Poly<N>& p, V2 d) {
     p.x[i] = x.x; p.x[i + 1] = x.y; p.y[i] = y.x; p.y[i + 1] = y.y;
   }
   if (N & 1) { p.x[N - 1] = p.x[N - 1] + d.x; p.y[N - 1] = p.y[N - 1] + d.y; }
-#else
-#pragma unroll
-  for (int i = 0; i < N; i++) { p.x[i] = p.x[i] + d.x; p.y[i] = p.y[i] + d.y; }
-#endif
   p.cx = p.cx + d.x;
   p.cy = p.cy + d.y;
 }
@@ -163,7 +152,6 @@ DEV void rotate(Poly<N>& p, float angle) {
   else sincos((double)angle, &sd, &cd);
   const float c = (float)cd, s = (float)sd;
   const float m11 = c, m12 = s, m21 = -s, m22 = c;
-#if WK_PACKED_ROT
   const pf2 cx = {p.cx, p.cx}, cy = {p.cy, p.cy}, z2 = {0.0f, 0.0f};
   const pf2 a11 = {m11, m11}, a12 = {m12, m12}, a21 = {m21, m21}, a22 = {m22, m22};
 #pragma unroll
@@ -182,16 +170,6 @@ DEV void rotate(Poly<N>& p, float angle) {
     p.x[i] = tx + p.cx;
     p.y[i] = ty + p.cy;
   }
-#else
-#pragma unroll
-  for (int i = 0; i < N; i++) {
-    float px = p.x[i] - p.cx, py = p.y[i] - p.cy;
-    float tx = (px * m11) + (py * m21) + 0.0f;
-    float ty = (px * m12) + (py * m22) + 0.0f;
-    p.x[i] = tx + p.cx;
-    p.y[i] = ty + p.cy;
-  }
-#endif
 }
 
 // BoundingBox.FindSignificantCorners + IsColliding (Skeleton.cs:133-176)
@@ -243,12 +221,11 @@ DEV void project2(float ax, float ay, const Poly<NA>& A, const Poly<NB>& B, floa
 // through v_pk_mul_f32 / v_pk_add_f32: two IEEE fp32 products / sums per instruction, the
 // same per-element operations as ax * x + ay * y (no FMA: -ffp-contract=off).  Measured
 // (bench A/B on one box): -2 % rollout time; Skeleton.Move / Rotate over vertex pairs
-// (WK_PACKED_ROT) another -0.7 %; packing per (x, y) pair instead cost +25 % (register
+// (move, rotate) another -0.7 %; packing per (x, y) pair instead cost +25 % (register
 // shuffles), packing the contact-face projections changed nothing.
 template <int N>
 DEV void proj_minmax(const Poly<N>& P, float ax, float ay, float& mn, float& mx) {
   float v[N];
-#if WK_PACKED_PROJ
   const pf2 a2 = {ax, ax}, b2 = {ay, ay};
 #pragma unroll
   for (int i = 0; i + 1 < N; i += 2) {
@@ -257,10 +234,6 @@ DEV void proj_minmax(const Poly<N>& P, float ax, float ay, float& mn, float& mx)
     v[i + 1] = q.y;
   }
   if (N & 1) v[N - 1] = ax * P.x[N - 1] + ay * P.y[N - 1];
-#else
-#pragma unroll
-  for (int i = 0; i < N; i++) v[i] = ax * P.x[i] + ay * P.y[i];
-#endif
   mn = FLT_MAX; mx = -FLT_MAX;
 #pragma unroll
   for (int i = 0; i < N; i++) { mn = __builtin_fminf(mn, v[i]); mx = __builtin_fmaxf(mx, v[i]); }
@@ -751,13 +724,7 @@ DEV int contact_points_floor(const Poly<NA>& A, const EdgeAxes<NA>& AXA, V2 norm
   V2 ra, rb, rmax, rd, ia, ib, imax, id;
   if constexpr (S > 0) significant_face_lds<NA, S>(A, AXA, normal, rec, ra, rb, rmax, rd);
   else significant_face_ax(A, AXA, normal, ra, rb, rmax, rd);
-#if WK_FLOOR_FACE_LOOP
-  Poly<4> F;
-  floor_poly(F);
-  significant_face_ax(F, floor_axes(), vneg(normal), ia, ib, imax, id);
-#else
   floor_face_ax(vneg(normal), ia, ib, imax, id);
-#endif
   return contact_clip(ra, rb, rmax, rd, ia, ib, imax, id, normal, c0, c1);
 }
 

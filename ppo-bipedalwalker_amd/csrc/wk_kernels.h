@@ -82,16 +82,6 @@ struct AdamArgs {
   float c1, c2, beta1, beta2, bc1, bc2, alpha, eps;
 };
 
-// the single-GPU minibatch tail fused into the matrix-core gradient kernels (wk_tail.h grad_tail)
-struct GradTail {
-  uint32_t* cnt;     // the context's monotone block-arrival counter (device)
-  uint32_t target;   // its value once every block of this launch has arrived
-  int on;            // 0: no tail (the separate reduction launch follows); 1 release / acquire, 2 sc1 hand-off
-  float* grad;       // the summed slab
-  uint32_t* err;     // set if a tail block's bounded wait ran out
-  AdamArgs a;
-};
-
 struct GradArgs {
   const float* W;        // params
   const float* Wz;       // the same params in the matrix-core operand order (wk_mfma_layout.h)
@@ -111,7 +101,6 @@ struct GradArgs {
   float lp_const;        // -ln(std) - ln(sqrt(2 pi))
   float upper, lower;    // 1 + eps, 1 - eps
   float* partial;        // [nblocks][SLAB]
-  GradTail tail;         // (matrix-core kernels ws / tp / tp1)
 };
 
 // gradient + critic diag, actor diag, skipped, then zero pads to a multiple of 4 floats (16-byte
@@ -184,7 +173,12 @@ struct XchArgs {
   uint64_t timeout_ticks;              // the bounded wait (s_memrealtime ticks)
   uint32_t t;                          // this minibatch's Adam step (with a.W)
   AdamArgs a;                          // a.W == null: exchange only (gradient-only calls)
+  uint64_t* stamps;                    // null, or this launch's [blocks][XCH_POINTS] clock stamps
 };
+// exchange timing (wk_comm_xch_profile): per block, the 100 MHz constant clock at entry, slab
+// published, every peer's flag seen, exit
+enum : int { XCH_POINTS = 4 };
+int xch_blocks();
 size_t xch_region_bytes();
 hipError_t launch_reduce_xch_adam(const XchArgs& x, hipStream_t s);
 hipError_t launch_normalize(float* x, int n, float eps, hipStream_t s);

@@ -19,6 +19,7 @@
 #include "wk_device.h"
 #include "wk_kernels.h"
 #include "wk_mfma_layout.h"
+#include "wk_region_prof.h"
 
 // Build parts (the Makefile compiles this file seven times, in parallel): kernels are
 // templates instantiated where the host shims at the end launch them, so each part holds the
@@ -30,53 +31,10 @@
 #endif
 #define WK_PART(k) (WK_PHYS_PART == 0 || WK_PHYS_PART == (k))
 
-#ifndef WK_ENV_WAVES
-#define WK_ENV_WAVES 2
-#endif
-#if WK_ENV_WAVES > 1
-#define WK_ENV_WPE __attribute__((amdgpu_waves_per_eu(WK_ENV_WAVES, WK_ENV_WAVES)))
-#else
-#define WK_ENV_WPE
-#endif
+// two waves per SIMD for the one- and 16-lane kernels (three: 168 VGPRs, spills, slower)
+#define WK_ENV_WPE __attribute__((amdgpu_waves_per_eu(2, 2)))
 
 namespace wk {
-
-// Optional per-region wave-time profile (build with -DWK_REGION_PROF; scripts/region_prof.py).
-// Wave-level: every mark is executed by the lanes that run the code it ends,
-// and the wave's FIRST ACTIVE lane charges the s_memtime delta since the wave's previous mark --
-// whichever lanes executed that one -- to the region the mark names, in a per-wave LDS record.
-// So a region's time is the time the WAVE spent executing it (whatever its lane mask), and 'other'
-// is only the code between regions (slot selection, joins, the env-step tail).  Each mark also
-// adds the number of active lanes, so lanes / count is the region's mean active lanes.
-enum { RP_JOINT, RP_INTEG, RP_AABB_LL, RP_AABB_LF, RP_AABB_BF, RP_SAT_LL, RP_SAT_LF, RP_SAT_BF,
-       RP_CON_LL, RP_CON_LF, RP_CON_BF, RP_IMP_LL, RP_IMP_LF, RP_IMP_BF, RP_POLICY, RP_OTHER,
-       RP_Q_PUT, RP_Q_B1, RP_Q_WORK, RP_Q_B2, RP_Q_GET, RP_N };  // (RP_Q_*: the pooled stages)
-#ifdef WK_REGION_PROF
-static __device__ unsigned long long g_region_prof[3 * RP_N];  // ticks, lane sums, counts
-struct WaveProf { unsigned long long acc[RP_N]; unsigned long long lanes[RP_N]; unsigned cnt[RP_N]; unsigned long long t; };
-struct RegionProf { WaveProf* w; };
-// deps: values the region computes -- the empty asm makes them ready before the stamp, so the
-// scheduler cannot sink the region's arithmetic past its mark into the next region
-DEV void rp_dep(float v) { asm volatile("" ::"v"(v)); }
-template <class... T>
-DEV void rp_mark(RegionProf* p, int r, T... deps) {
-  if (!p) return;
-  (rp_dep((float)deps), ...);
-  const uint64_t ex = __builtin_amdgcn_read_exec();
-  const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  if (lane == __builtin_ffsll((long long)ex) - 1) {
-    const uint64_t t = __builtin_amdgcn_s_memtime();
-    p->w->acc[r] += t - p->w->t;
-    p->w->t = t;
-    p->w->lanes[r] += (unsigned long long)__builtin_popcountll(ex);
-    p->w->cnt[r] += 1u;
-  }
-}
-#else
-struct RegionProf {};
-template <class... T>
-DEV void rp_mark(RegionProf*, int, T...) {}
-#endif
 
 struct EnvState {
   Poly<6> lll, llu, rll, rlu;
@@ -220,25 +178,6 @@ DEV void get_obs(const EnvState& s, float o[12]) {
   o[11] = s.drlu.th;
 }
 
-// Differential cost probes (build with -DWK_DUP=k, scripts/dup_probe.sh): region k runs a
-// second time on inputs perturbed by an opaque zero, results kept alive but unused.
-#ifdef WK_DUP
-DEV float opaque_zero() { float z; asm volatile("v_mov_b32 %0, 0" : "=v"(z)); return z; }
-DEV void sink(float v) { asm volatile("" ::"v"(v)); }
-template <int N>
-DEV Poly<N> perturbed(const Poly<N>& p) {
-  Poly<N> q = p;
-  const float z = opaque_zero();
-#pragma unroll
-  for (int i = 0; i < N; i++) { q.x[i] = q.x[i] + z; q.y[i] = q.y[i] + z; }
-  q.cx = q.cx + z; q.cy = q.cy + z;
-  return q;
-}
-#define DUP(k, ...) do { if (WK_DUP == (k)) { __VA_ARGS__ } } while (0)
-#else
-#define DUP(k, ...) do {} while (0)
-#endif
-
 // ---------------- quad mapping helpers (L = 4: two lanes per leg) ----------------
 // The lane pair of a leg (halves 0 and 1: quad_perm [2,3,0,1] partners) holds the same leg
 // state and splits the heavy halves of its pairs; each half ends with the other's results
@@ -367,7 +306,6 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
     ov = mnx < b1x && mxx > b0x && mny < b1y && mxy > b0y;
   }
   rp_mark(rp, RP_AABB_LL + EVK, ov ? 1.0f : 0.0f);
-  DUP(1, { const auto Ap = perturbed(A); sink(aabb_overlap(Ap, B) ? 1.0f : 0.0f); });
   if (!ov) return;
   if (ec) ec[EV_AABB_LL + EVK]++;
   if (TRACE && tr && pi >= 0) tr->aabb_hit[pi] = 1;
@@ -389,8 +327,6 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   else if constexpr (KEEP) hit = sat<NA, NB, false, true>(A, B, n, depth, &axa, &axb);
   else hit = sat<NA, NB, GENERIC, true>(A, B, n, depth);
   rp_mark(rp, RP_SAT_LL + EVK, depth, n.x, n.y, hit ? 1.0f : 0.0f);
-  DUP(2, { const auto Ap = perturbed(A); V2 n2; float d2;
-           const bool h2 = sat(Ap, B, n2, d2); sink(n2.x); sink(n2.y); sink(d2); sink(h2 ? 1.0f : 0.0f); });
   if (!hit) return;
   if (ec) ec[EV_SAT_LL + EVK]++;
   V2 c0, c1;
@@ -400,8 +336,6 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   else if constexpr (KEEP) nc = contact_points_ax<NA, NB, FS>(A, axa, B, axb, n, c0, c1, frec);
   else nc = contact_points<NA, NB, GENERIC>(A, B, n, c0, c1);
   rp_mark(rp, RP_CON_LL + EVK, c0.x, c0.y, c1.x, c1.y, (float)nc);
-  DUP(3, { const auto Ap = perturbed(A); V2 e0, e1;
-           const int k2 = contact_points(Ap, B, n, e0, e1); sink(e0.x); sink(e1.y); sink((float)k2); });
   if (TRACE && tr && pi >= 0) {
     tr->sat_hit[pi] = 1;
     tr->n_contacts[pi] = (uint8_t)nc;
@@ -447,14 +381,6 @@ DEV void resolve_pair(Poly<NA>& A, Dyn& dA, const Mat& mA, Poly<NB>& B, Dyn& dB,
   apply_impulses<BSTATIC>(bA, bB, n, j, rA, rB);
   apply_impulses<BSTATIC>(bA, bB, tangent, jf, rAF, rBF);
   rp_mark(rp, RP_IMP_LL + EVK, dA.vx, dA.vy, dA.w, dB.vx, dB.vy, dB.w);
-  DUP(4, { Dyn dA2 = dA, dB2 = dB; const float z = opaque_zero();
-           Body cA{A.cx + z, A.cy, &dA2, mA.im, mA.ii}; Body cB{B.cx, B.cy, &dB2, mB.im, mB.ii};
-           V2 sA, sB, sAF, sBF;
-           const float j2 = calc_impulse(cA, cB, contact, 1.0f + e, n, sA, sB);
-           const float jf2 = calc_impulse(cA, cB, contact, mu, tangent, sAF, sBF);
-           apply_impulses<BSTATIC>(cA, cB, n, j2, sA, sB);
-           apply_impulses<BSTATIC>(cA, cB, tangent, jf2, sAF, sBF);
-           sink(dA2.vx); sink(dA2.w); sink(dB2.vy); });
 }
 
 // Joint.Step (Objects/RigidBodies/Joint.cs:31-41); ResolveJoint swaps the bodies (:40)
@@ -1048,11 +974,9 @@ DEV void get_obs_side(const SideState& s, int side, float o[12]) {
 // by the left lane): integrate, then its only candidate, the floor.  It reads and writes the torso
 // alone (its leg pairs are associated bodies, Walker.cs:202-209), and no leg step reads the torso,
 // so it commutes with the legs' steps that precede it in the list [LLL, LLU, Body, RLL, RLU]:
-// WK_TORSO_EARLY (default) runs it right after the joints, in the lower leg's integrate's basic
-// block, where the two independent integrate chains interleave (bit-identical either way).
-#ifndef WK_TORSO_EARLY
-#define WK_TORSO_EARLY 1
-#endif
+// substep_side runs it right after the joints, in the lower leg's integrate's basic
+// block, where the two independent integrate chains interleave (bit-identical either way; round 5,
+// within noise).
 template <bool TRACE, bool ROUGH, int TS>
 DEV void torso_step(SideState& s, const Mat& mb, float dt, float adx, float ady, PairTraceDev* tr,
                     int side, RegionProf* rp, const float* ter) {
@@ -1086,9 +1010,6 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
   const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};
   // joints [bodyJointLeft, bodyJointRight, leftJoint, rightJoint] (Walker.cs:182-187)
   if (side == 0) joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.up, s.dup, mp, tr, 0);
-  DUP(5, { auto b2 = perturbed(s.body); auto u2 = s.up; Dyn db2 = s.dbody, du2 = s.dup;
-           joint_step<5, 6, 1, 4, false>(b2, db2, mb, u2, du2, mp, nullptr, 0);
-           sink(b2.cx); sink(u2.cy); sink(db2.w); sink(du2.vx); });
   bcast_torso<0xA0>(s.body, s.dbody);
   if (side == 1) joint_step<5, 6, 1, 4, TRACE>(s.body, s.dbody, mb, s.up, s.dup, mp, tr, 1);
   bcast_torso<0xF5>(s.body, s.dbody);
@@ -1098,13 +1019,9 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
   // floor-first after a reset, floor-last in episode 0: three slots keep a wave with
   // both kinds of walkers at three pair evaluations instead of four
   const int pb = side ? 5 : 0;
-#if WK_TORSO_EARLY
   torso_step<TRACE, ROUGH, TS>(s, mb, dt, adx, ady, tr, side, rp, ter);
-#endif
   integrate(s.lo, s.dlo, dt, adx, ady);
   rp_mark(rp, RP_INTEG, s.lo.x[0], s.lo.y[3], s.lo.x[5], s.dlo.th);
-  DUP(6, { auto l2 = perturbed(s.lo); Dyn d2 = s.dlo; integrate(l2, d2, dt, adx, ady);
-           sink(l2.x[0]); sink(l2.y[5]); sink(d2.th); });
 #pragma unroll
   for (int q = 0; q < 3; q++) {  // [floor if post], other segment, [floor if episode 0]
     if (q == 1) resolve_pair<6, 6, false, TRACE, 1, false, Q, FS>(s.lo, s.dlo, mp, s.up, s.dup, mp, s.clo, tr, pb + 0, half, rp, nullptr, frec);
@@ -1125,325 +1042,12 @@ DEV void substep_side(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
     }
     rp_mark(rp, RP_OTHER);
   }
-#if !WK_TORSO_EARLY
-  torso_step<TRACE, ROUGH, TS>(s, mb, dt, adx, ady, tr, side, rp, ter);
-#endif
   rp_mark(rp, RP_OTHER);
 }
 
 DEV bool side_finite(const SideState& s) {  // this side's legs and the torso (see state_finite)
   const float acc = nonfinite_acc(s.lo, s.dlo) + nonfinite_acc(s.up, s.dup) + nonfinite_acc(s.body, s.dbody);
   return acc == 0.0f;
-}
-
-// ---------------- block-pooled contact stages (pair mapping, flat floor; round 5) ----------------
-// The wave-level region probe (profiles/r05_region_prof.txt) put half of a pair-mapping wave's
-// time into the leg pairs' narrow-phase tails, run wave-wide for a few lanes: per wave-substep the
-// leg-leg contact clipping + impulses 22 % of the time at 17.9 of 64 lanes, the leg-floor SAT +
-// contacts + impulses 16 % at 15.4 lanes.  A pooled stage compacts those tails over the block's
-// four waves (RigidBody.cs:66-96 / ContactPoints.cs:13-53 / Impulses.cs:12-28, unchanged order):
-// every lane decides its own candidate (bounding box, and for leg-leg the SAT: dense), the lanes
-// that go on write their pair as a task into an LDS queue -- a wave ballot + prefix (mbcnt) for the
-// slot within the wave and one LDS atomic per wave for the wave's base -- one block barrier, then
-// the queue's tasks are processed densely by as few waves as they fill (task t by lane t % 64 of
-// wave (t / 64 + rot) % 4: ~72 leg-leg tasks take two waves instead of four, ~60 floor tasks one),
-// a second barrier, and every owner reads its result back by its slot.  A task is a pure function
-// of its inputs, so whichever lane computes it the results are the owner's own bits.
-// The 36-KB region is shared over an env-step: [0, 1536) float4 the legs parked across the policy
-// ([record][lane]), [1536, 2304) the policy's observation tiles; during the substeps the task
-// queues (floor: 7 float4 per task, leg-leg: 17) below RES and both queues' results (2 float4 per
-// task) from RES.  Tasks and results live in disjoint parts, so a stage's puts never meet the
-// previous stage's late result reads; a block barrier before and after the policy section keeps
-// the stash / tiles apart from the queues.
-#ifndef WK_POOL
-#define WK_POOL 0  // bit 0: the leg-floor slots, bit 1: the leg-leg pairs (0: the per-lane kernel)
-#endif
-namespace pool {
-enum : int {
-  F4 = 2304,            // float4s of the region (36 KB)
-  STASH = 0, POL = 1536, RES = 1792,
-  FT = 7, FCAP = 256,   // floor tasks in [0, 1792)
-  LT = 17, LCAP = 105   // leg-leg tasks in [0, 1785)
-};
-static_assert(FT * FCAP <= RES && LT * LCAP <= RES && RES + 2 * FCAP <= F4, "queue layout");
-}  // namespace pool
-
-// One pooled stage: block-collective (every thread of the block calls it from converged code).
-// cnt: two LDS counters used alternately by consecutive stages (a stage clears the next one's
-// after its first barrier, when every reader of that counter's last use has passed).
-template <int TS, int CAP, class PUT, class WORK, class GET>
-DEV void pool_run(bool need, float4* __restrict__ q, int* cnt, uint32_t& seq, PUT&& put, WORK&& work,
-                  GET&& get, RegionProf* rp = nullptr) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t bal = __ballot(need);
-  int* const c = cnt + (seq & 1u);
-  int base = 0;
-  if (bal != 0ull) {  // wave-uniform: one LDS atomic per wave reserves its slots
-    int got = 0;
-    if (lane == 0) got = atomicAdd(c, __builtin_popcountll(bal));
-    base = __builtin_amdgcn_readfirstlane(got);
-  }
-  const int idx = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-  if (need && idx < CAP) put(q + idx * TS);
-  rp_mark(rp, RP_Q_PUT);
-  __syncthreads();
-  const int total = *(volatile int*)c;
-  rp_mark(rp, RP_Q_B1, (float)total);
-  if (threadIdx.x == 0) cnt[(seq + 1u) & 1u] = 0;
-  const int rot = (int)((seq + blockIdx.x) & 3u);
-  seq++;
-  if (total == 0) return;  // block-uniform
-  const int t = (((wave + rot) & 3) << 6) | lane;  // this lane's slot as a worker
-  for (int done = 0;;) {
-    const int m = total - done < CAP ? total - done : CAP;
-    if (t < m) work(q + t * TS, q + pool::RES + 2 * t);
-    rp_mark(rp, RP_Q_WORK);
-    __syncthreads();
-    rp_mark(rp, RP_Q_B2);
-    if (need && idx >= done && idx < done + CAP) get(q + pool::RES + 2 * (idx - done));
-    rp_mark(rp, RP_Q_GET);
-    done += CAP;
-    if (done >= total) break;
-    __syncthreads();  // (overflow round) every result read before the next round reuses the slots
-    if (need && idx >= done && idx < done + CAP) put(q + (idx - done) * TS);
-    __syncthreads();
-  }
-}
-
-// RigidBody.ResolveCollisions' impulse tail (Impulses.cs:12-28) on a pair whose MoveObjects has
-// run (post-correction centroids), as resolve_pair's H = 1 path
-template <bool BSTATIC>
-DEV void pair_impulses(float acx, float acy, Dyn& dA, const Mat& mA, float bcx, float bcy, Dyn& dB,
-                       const Mat& mB, V2 n, int nc, V2 c0, V2 c1) {
-  const float e = net_maxf(mA.e, mB.e);
-  const float mu = net_minf(mA.mu, mB.mu);
-  const V2 contact = nc == 2 ? vdiv(vadd(c0, c1), 2.0f) : c0;
-  Body bA{acx, acy, &dA, mA.im, mA.ii};
-  Body bB{bcx, bcy, &dB, mB.im, mB.ii};
-  V2 rA, rB, rAF, rBF;
-  const V2 tangent = mk(-n.y, n.x);
-  const float j = calc_impulse(bA, bB, contact, 1.0f + e, n, rA, rB);
-  const float jf = calc_impulse(bA, bB, contact, mu, tangent, rAF, rBF);
-  apply_impulses<BSTATIC>(bA, bB, n, j, rA, rB);
-  apply_impulses<BSTATIC>(bA, bB, tangent, jf, rAF, rBF);
-}
-
-DEV void put_poly6(float4* q, const Poly<6>& A) {
-  q[0] = make_float4(A.x[0], A.x[1], A.x[2], A.x[3]);
-  q[1] = make_float4(A.x[4], A.x[5], A.y[0], A.y[1]);
-  q[2] = make_float4(A.y[2], A.y[3], A.y[4], A.y[5]);
-}
-DEV void get_poly6(const float4* q, Poly<6>& A) {
-  const float4 a = q[0], b = q[1], c = q[2];
-  A.x[0] = a.x; A.x[1] = a.y; A.x[2] = a.z; A.x[3] = a.w;
-  A.x[4] = b.x; A.x[5] = b.y; A.y[0] = b.z; A.y[1] = b.w;
-  A.y[2] = c.x; A.y[3] = c.y; A.y[4] = c.z; A.y[5] = c.w;
-}
-DEV void put_axes6(float4* q, const EdgeAxes<6>& X) {
-  q[0] = make_float4(X.x[0], X.x[1], X.x[2], X.x[3]);
-  q[1] = make_float4(X.x[4], X.x[5], X.y[0], X.y[1]);
-  q[2] = make_float4(X.y[2], X.y[3], X.y[4], X.y[5]);
-}
-DEV void get_axes6(const float4* q, EdgeAxes<6>& X) {
-  const float4 a = q[0], b = q[1], c = q[2];
-  X.x[0] = a.x; X.x[1] = a.y; X.x[2] = a.z; X.x[3] = a.w;
-  X.x[4] = b.x; X.x[5] = b.y; X.y[0] = b.z; X.y[1] = b.w;
-  X.y[2] = c.x; X.y[3] = c.y; X.y[4] = c.z; X.y[5] = c.w;
-}
-
-// leg segment vs the flat floor, after its bounding box overlapped (the owner set Collided):
-// sat_floor, contact_points_floor, MoveObjects, impulses -- resolve_pair<6, 4, true, ...>'s tail.
-// Result: the MoveObjects translation (applied by the owner iff the SAT hit) and the new velocities.
-DEV void floor_task_put(float4* q, const Poly<6>& A, const Dyn& d, const Mat& m, float mnx, float mny,
-                        float mxx, float mxy) {
-  put_poly6(q, A);
-  q[3] = make_float4(A.cx, A.cy, d.vx, d.vy);
-  q[4] = make_float4(d.w, m.im, m.ii, m.e);
-  q[5] = make_float4(m.mu, mnx, mny, mxx);
-  q[6] = make_float4(mxy, 0.0f, 0.0f, 0.0f);
-}
-DEV void floor_task_work(const float4* q, float4* r) {
-  Poly<6> A;
-  get_poly6(q, A);
-  const float4 q3 = q[3], q4 = q[4], q5 = q[5], q6 = q[6];
-  A.cx = q3.x; A.cy = q3.y;
-  Dyn d;
-  d.vx = q3.z; d.vy = q3.w; d.w = q4.x; d.th = 0.0f;
-  const Mat m{q4.y, q4.z, q4.w, q5.x};
-  Poly<4> fl;
-  floor_poly(fl);
-  V2 n;
-  float depth;
-  EdgeAxes<6> axa;
-  const bool hit = sat_floor<6, true>(A, fl, q5.y, q5.z, q5.w, q6.x, n, depth, &axa);
-  V2 mv = mk(0.0f, 0.0f);
-  if (hit) {
-    V2 c0, c1;
-    const int nc = contact_points_floor<6>(A, axa, n, c0, c1);
-    mv = vmul(n, depth);
-    const float cx = A.cx + mv.x, cy = A.cy + mv.y;  // Skeleton.Move's centroid
-    if (nc > 0) {
-      Dyn dfl;
-      zero_dyn(dfl);
-      const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};
-      pair_impulses<true>(cx, cy, d, m, fl.cx, fl.cy, dfl, mf, n, nc, c0, c1);
-    }
-  }
-  r[0] = make_float4(mv.x, mv.y, d.vx, d.vy);
-  r[1] = make_float4(d.w, hit ? 1.0f : 0.0f, 0.0f, 0.0f);
-}
-
-// leg segment A vs the other segment B of the same leg after the SAT hit (the owner ran AABB +
-// SAT and applies MoveObjects itself): contact_points_ax from the SAT's axes, then the impulses
-// on the post-correction centroids.  Result: both segments' new velocities.
-DEV void ll_task_put(float4* q, const Poly<6>& A, const Poly<6>& B, const EdgeAxes<6>& axa,
-                     const EdgeAxes<6>& axb, V2 n, float depth, const Dyn& dA, const Dyn& dB,
-                     const Mat& m) {
-  put_poly6(q, A);
-  q[3] = make_float4(A.cx, A.cy, B.cx, B.cy);
-  put_poly6(q + 4, B);
-  put_axes6(q + 7, axa);
-  put_axes6(q + 10, axb);
-  q[13] = make_float4(n.x, n.y, depth, m.im);
-  q[14] = make_float4(dA.vx, dA.vy, dA.w, m.ii);
-  q[15] = make_float4(dB.vx, dB.vy, dB.w, m.e);
-  q[16] = make_float4(m.mu, 0.0f, 0.0f, 0.0f);
-}
-DEV void ll_task_work(const float4* q, float4* r) {
-  Poly<6> A, B;
-  get_poly6(q, A);
-  get_poly6(q + 4, B);
-  const float4 q3 = q[3], q13 = q[13], q14 = q[14], q15 = q[15], q16 = q[16];
-  A.cx = q3.x; A.cy = q3.y; B.cx = q3.z; B.cy = q3.w;
-  EdgeAxes<6> axa, axb;
-  get_axes6(q + 7, axa);
-  get_axes6(q + 10, axb);
-  const V2 n = mk(q13.x, q13.y);
-  const float depth = q13.z;
-  const Mat m{q13.w, q14.w, q15.w, q16.x};
-  Dyn dA, dB;
-  dA.vx = q14.x; dA.vy = q14.y; dA.w = q14.z; dA.th = 0.0f;
-  dB.vx = q15.x; dB.vy = q15.y; dB.w = q15.z; dB.th = 0.0f;
-  V2 c0, c1;
-  const int nc = contact_points_ax<6, 6>(A, axa, B, axb, n, c0, c1);
-  if (nc > 0) {
-    const V2 tA = vdiv(vmul(n, depth), 2.0f), tB = vdiv(vmul(vneg(n), depth), 2.0f);
-    pair_impulses<false>(A.cx + tA.x, A.cy + tA.y, dA, m, B.cx + tB.x, B.cy + tB.y, dB, m, n, nc, c0, c1);
-  }
-  r[0] = make_float4(dA.vx, dA.vy, dA.w, dB.vx);
-  r[1] = make_float4(dB.vy, dB.w, 0.0f, 0.0f);
-}
-
-struct PoolCtx {
-  float4* q;        // the block's region
-  int* cnt;         // two LDS counters
-  uint32_t seq;     // stages so far (block-uniform)
-  bool blk_post;    // some walker of the block is past its first episode (floor-first slot)
-  bool blk_ep0;     // some walker of the block is in its first episode (floor-last slot)
-};
-
-// one floor candidate slot of a leg segment, pooled; mine: this walker takes the floor in this slot
-DEV void floor_stage(Poly<6>& A, Dyn& dA, bool& colA, const Mat& m, bool mine, PoolCtx& pc,
-                     RegionProf* rp) {
-  float mnx, mny, mxx, mxy;
-  aabb(A, mnx, mny, mxx, mxy);
-  const bool ov = mine && mnx < 1050.0f && mxx > -50.0f && mny < 1050.0f && mxy > 900.0f;
-  if (ov) colA = true;  // body._isFloor -> Collided = true at the bounding box (:75)
-  rp_mark(rp, RP_AABB_LF, ov ? 1.0f : 0.0f);
-  pool_run<pool::FT, pool::FCAP>(
-      ov, pc.q, pc.cnt, pc.seq, [&](float4* t) { floor_task_put(t, A, dA, m, mnx, mny, mxx, mxy); },
-      floor_task_work,
-      [&](const float4* r) {
-        const float4 r0 = r[0], r1 = r[1];
-        if (r1.y != 0.0f) move(A, mk(r0.x, r0.y));
-        dA.vx = r0.z; dA.vy = r0.w; dA.w = r1.x;
-      }, rp);
-  rp_mark(rp, RP_CON_LF, dA.vx, dA.w);
-}
-
-// the leg-leg candidate of segment A against segment B (A's own list step), pooled after the SAT
-DEV void ll_stage(Poly<6>& A, Dyn& dA, Poly<6>& B, Dyn& dB, const Mat& m, PoolCtx& pc, RegionProf* rp) {
-  float a0x, a0y, a1x, a1y, b0x, b0y, b1x, b1y;
-  aabb(A, a0x, a0y, a1x, a1y);
-  aabb(B, b0x, b0y, b1x, b1y);
-  const bool ov = a0x < b1x && a1x > b0x && a0y < b1y && a1y > b0y;
-  rp_mark(rp, RP_AABB_LL, ov ? 1.0f : 0.0f);
-  V2 n = mk(0.0f, 0.0f);
-  float depth = 0.0f;
-  EdgeAxes<6> axa, axb;
-  bool hit = false;
-  if (ov) hit = sat<6, 6, false, true>(A, B, n, depth, &axa, &axb);
-  rp_mark(rp, RP_SAT_LL, depth, n.x, n.y, hit ? 1.0f : 0.0f);
-  pool_run<pool::LT, pool::LCAP>(
-      hit, pc.q, pc.cnt, pc.seq,
-      [&](float4* t) {
-        ll_task_put(t, A, B, axa, axb, n, depth, dA, dB, m);
-        move(A, vdiv(vmul(n, depth), 2.0f));  // MoveObjects (:99-113): both segments move
-        move(B, vdiv(vmul(vneg(n), depth), 2.0f));
-      },
-      ll_task_work,
-      [&](const float4* r) {
-        const float4 r0 = r[0], r1 = r[1];
-        dA.vx = r0.x; dA.vy = r0.y; dA.w = r0.z;
-        dB.vx = r0.w; dB.vy = r1.x; dB.w = r1.y;
-      }, rp);
-  rp_mark(rp, RP_CON_LL, dA.vx, dA.w, dB.w);
-}
-
-// a floor slot / the leg-leg pair of a segment, pooled (WK_POOL bit 0 / bit 1) or per lane
-template <bool POOLED>
-DEV void floor_slot(Poly<6>& A, Dyn& dA, bool& colA, const Mat& m, bool mine, PoolCtx& pc,
-                    RegionProf* rp) {
-  if constexpr (POOLED) {
-    floor_stage(A, dA, colA, m, mine, pc, rp);
-  } else if (mine) {
-    Poly<4> fl;
-    floor_poly(fl);
-    Dyn dfl;
-    zero_dyn(dfl);
-    const Mat mf{0.0f, 0.0f, 0.3f, 1.0f};
-    resolve_pair<6, 4, true, false, 1>(A, dA, m, fl, dfl, mf, colA, nullptr, -1, 0, rp);
-  }
-}
-template <bool POOLED>
-DEV void ll_slot(Poly<6>& A, Dyn& dA, bool& colA, Poly<6>& B, Dyn& dB, const Mat& m, PoolCtx& pc,
-                 RegionProf* rp) {
-  if constexpr (POOLED) ll_stage(A, dA, B, dB, m, pc, rp);
-  else resolve_pair<6, 6, false, false, 1>(A, dA, m, B, dB, m, colA, nullptr, -1, 0, rp);
-}
-
-// substep_side for the pair mapping with the pooled stages (no traces: the TRACE kernels keep the
-// per-lane path); every slot runs in block-uniform control flow
-template <int PM>  // WK_POOL: bit 0 the floor slots, bit 1 the leg-leg pairs
-DEV void substep_pool(SideState& s, const Mat& mp, const Mat& mb, float dt, float adx, float ady,
-                      int side, PoolCtx& pc, RegionProf* rp) {
-  constexpr bool PF = (PM & 1) != 0, PL = (PM & 2) != 0;
-  rp_mark(rp, RP_OTHER);
-  if (side == 0) joint_step<5, 6, 1, 4, false>(s.body, s.dbody, mb, s.up, s.dup, mp, nullptr, 0);
-  bcast_torso<0xA0>(s.body, s.dbody);
-  if (side == 1) joint_step<5, 6, 1, 4, false>(s.body, s.dbody, mb, s.up, s.dup, mp, nullptr, 1);
-  bcast_torso<0xF5>(s.body, s.dbody);
-  joint_step<6, 6, 2, 3, false>(s.up, s.dup, mp, s.lo, s.dlo, mp, nullptr, 2 + side);
-  rp_mark(rp, RP_JOINT, s.dup.w, s.dlo.w, s.up.x[0], s.lo.x[0], s.dbody.w, s.body.x[0]);
-#if WK_TORSO_EARLY
-  torso_step<false, false, 1>(s, mb, dt, adx, ady, nullptr, side, rp, nullptr);
-#endif
-  integrate(s.lo, s.dlo, dt, adx, ady);
-  rp_mark(rp, RP_INTEG, s.lo.x[0], s.lo.y[3], s.lo.x[5], s.dlo.th);
-  // [floor if post], other segment, [floor if episode 0] (RigidBody.cs:66-96 list order)
-  if (pc.blk_post) floor_slot<PF>(s.lo, s.dlo, s.clo, mp, s.post, pc, rp);
-  ll_slot<PL>(s.lo, s.dlo, s.clo, s.up, s.dup, mp, pc, rp);
-  if (pc.blk_ep0) floor_slot<PF>(s.lo, s.dlo, s.clo, mp, !s.post, pc, rp);
-  integrate(s.up, s.dup, dt, adx, ady);
-  rp_mark(rp, RP_INTEG, s.up.x[0], s.up.y[3], s.up.x[5], s.dup.th);
-  if (pc.blk_post) floor_slot<PF>(s.up, s.dup, s.cup, mp, s.post, pc, rp);
-  ll_slot<PL>(s.up, s.dup, s.cup, s.lo, s.dlo, mp, pc, rp);
-  if (pc.blk_ep0) floor_slot<PF>(s.up, s.dup, s.cup, mp, !s.post, pc, rp);
-#if !WK_TORSO_EARLY
-  torso_step<false, false, 1>(s, mb, dt, adx, ady, nullptr, side, rp, nullptr);
-#endif
-  rp_mark(rp, RP_OTHER);
 }
 
 // PPOAgent.SampleActions / GetValueEstimate forward passes (NeuralNetwork.FeedForward,
@@ -1457,32 +1061,18 @@ DEV void substep_pool(SideState& s, const Mat& mp, const Mat& mb, float dt, floa
 typedef float pf4 __attribute__((ext_vector_type(4)));
 // an opaque copy of a lane value: the address arithmetic built on it is redone where it is used
 // instead of being strength-reduced into per-lane 64-bit pointers that live across a loop
-#ifndef WK_OPAQUE
-#define WK_OPAQUE 1
-#endif
-#ifndef WK_OPQ_LOOP
-#define WK_OPQ_LOOP 1
-#endif
 DEV uint32_t lane_opaque(uint32_t v) {
-#if WK_OPAQUE
   asm volatile("" : "+v"(v));
-#endif
   return v;
 }
-#ifndef WK_TRAJ_NT
-// the trajectory rows as plain stores (1: non-temporal).  Written bytes per rollout launch at
-// 65,536 walkers (rollouts only, profiles/r05_write_probe.txt): non-temporal 439 MiB, plain 403
-// MiB against 384 MiB algorithmic (385 MiB with the identity lane order): a walker the lane order
-// moved into another wave writes into lines that wave fills, and plain stores let the L2 merge
-// those parts before the line is written back; the one-byte done rows likewise (their 32 bytes
-// per wave share a 128-byte line with three other waves).  Time unchanged.
-#define WK_TRAJ_NT 0
-#endif
+// the trajectory rows as plain stores.  Written bytes per rollout launch at 65,536 walkers
+// (rollouts only, profiles/r05_write_probe.txt): non-temporal 439 MiB, plain 403 MiB against 384
+// MiB algorithmic (385 MiB with the identity lane order): a walker the lane order moved into
+// another wave writes into lines that wave fills, and plain stores let the L2 merge those parts
+// before the line is written back; the one-byte done rows likewise (their 32 bytes per wave share
+// a 128-byte line with three other waves).  Time unchanged.
 template <typename T>
-DEV void st_row(T v, T* p) {
-  if (WK_TRAJ_NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
+DEV void st_row(T v, T* p) { *p = v; }
 DEV void st_row4(float* p, float a, float b, float c, float d) {
   const pf4 v = {a, b, c, d};
   st_row(v, (pf4*)p);
@@ -1582,25 +1172,13 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool wri
   wave_lds_sync();  // outputs read before the next env-step rewrites the tile
 }
 
-#ifndef WK_FACE_LDS
-#define WK_FACE_LDS 1  // the pair mapping's contact faces through LDS (significant_face_lds)
-#endif
-#ifndef WK_FACE_LDS_QUAD
-#define WK_FACE_LDS_QUAD 0  // ... and the quad mapping's (one block per CU: its 80 KB fit; off by default)
-#endif
-#ifndef WK_POLICY_STASH
-#define WK_POLICY_STASH 1  // the legs' vertices parked in the lane's face column over the policy
-#endif
-#ifndef WK_QUAD_WAVES
-#define WK_QUAD_WAVES 1  // waves per SIMD the quad mapping is built for
-#endif
 constexpr int SIDE_BLOCK = SIDE_BLOCK_THREADS;  // 4 waves: the policy's weight image is staged once per block
 // Q = 1: a lane pair per walker (L = 2); Q = 2: a lane quad (L = 4, side = lane bit 0, half =
 // lane bit 1), for shards of at most one wave per SIMD, where the split shortens each wave's
 // dependent chain -- with room for every register (one wave per SIMD: no spills)
 template <bool POLICY, bool RECORD, bool TRACE, int Q, bool ROUGH = false>
 __global__ __launch_bounds__(SIDE_BLOCK)
-__attribute__((amdgpu_waves_per_eu(Q == 2 ? WK_QUAD_WAVES : WK_ENV_WAVES, Q == 2 ? WK_QUAD_WAVES : WK_ENV_WAVES)))
+__attribute__((amdgpu_waves_per_eu(Q == 2 ? 1 : 2, Q == 2 ? 1 : 2)))  // (quad: one wave per SIMD)
 void k_env_side(EnvParams P, StepArgs A) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int side = tid & 1;
@@ -1621,37 +1199,25 @@ void k_env_side(EnvParams P, StepArgs A) {
   const int slot = eraw < n ? eraw : n - 1;
   const int e = A.order ? A.order[slot] : slot;
   const bool leader = side == 0 && half == 0 && active;
-  // POOL: the pooled contact stages (pair mapping, flat floor, no traces); their 36-KB region
-  // also holds the policy tiles and the legs' stash, so pol_lds / face_lds shrink to nothing
-  constexpr bool POOL = WK_POOL && Q == 1 && !ROUGH && !TRACE;
-  static_assert(!POOL || SIDE_BLOCK == 256, "the pool layout is for 4-wave blocks");
-  __shared__ float pol_lds[POLICY && !POOL ? (SIDE_BLOCK / 64) * 768 : 1];
+  __shared__ float pol_lds[POLICY ? (SIDE_BLOCK / 64) * 768 : 1];
   __shared__ float wz_lds[POLICY ? mf::WEND : 1];  // operand-order weights (41 KB, 2 blocks/CU)
-  __shared__ float4 pool_lds[POOL ? pool::F4 : 1];
-  __shared__ int pool_cnt[2];
   // RoughFloor: the walker's terrain heights 800 + Random.Next(0, 100) (Environment.cs:242-250),
   // [draw][walker of block]; the walker's lanes write the same values and read only its column
   constexpr int WPB = SIDE_BLOCK >> SH;
   __shared__ float ter_lds[ROUGH ? 11 * WPB : 1];
   // the pair mapping's contact faces (significant_face_lds): 6 float4 records per lane,
   // [record][lane of block] (24 KB per block; 2 blocks of 77 KB fit a CU's 160 KB -- not with the
-  // rough floor's terrain as well, which would leave one block per CU)
-  constexpr int FS = !POOL && (((Q == 1 && !ROUGH) || (Q == 2 && WK_FACE_LDS_QUAD)) && WK_FACE_LDS) ? SIDE_BLOCK : 0;
+  // rough floor's terrain as well, which would leave one block per CU).  The quad mapping keeps
+  // the select chains (its LDS build: bit-exact, 1 % slower, profiles/r04_face_lds_ab.txt)
+  constexpr int FS = (Q == 1 && !ROUGH) ? SIDE_BLOCK : 0;
   __shared__ float4 face_lds[FS ? 6 * SIDE_BLOCK : 1];
   // the rough floor's pair kernel has no face column (its terrain would push two blocks past the
   // CU's LDS); a 4-record column (16 KB per block, 2 x 75 KB fit) parks 16 of the legs' 24
   // vertex coordinates over the policy instead of leaving them to the spill
-#ifndef WK_ROUGH_STASH
-#define WK_ROUGH_STASH 1
-#endif
-  constexpr int RS = (!POOL && Q == 1 && ROUGH && WK_ROUGH_STASH) ? SIDE_BLOCK : 0;
+  constexpr int RS = (Q == 1 && ROUGH) ? SIDE_BLOCK : 0;
   __shared__ float4 rstash_lds[RS ? 4 * SIDE_BLOCK : 1];
-  // the legs' stash across the policy section: the face column, or the pool region's first part
-  constexpr int SS = POOL ? SIDE_BLOCK : FS;
-  PoolCtx pc{pool_lds, pool_cnt, 0u, true, true};
-  if constexpr (POOL) {
-    if (threadIdx.x < 2) pool_cnt[threadIdx.x] = 0;  // (read after the stages' first barrier)
-  }
+  // the legs' stash across the policy section: the face column
+  constexpr int SS = FS;
   const int wib = ((threadIdx.x >> 6) * wpw) + ((threadIdx.x & ((wpw << SH) - 1)) >> SH);
   const float* const ter = ter_lds + wib;
   if constexpr (ROUGH) {
@@ -1666,26 +1232,14 @@ void k_env_side(EnvParams P, StepArgs A) {
   }
   SideState s;
   load_side(s, A.st, e, side);
-  const float dx = A.dxoff[e];
   const MatConst mc = material(A.mat[e]);
   const Mat mp{mc.inv_mass, 0.001f * mc.inv_mass, mc.restitution, mc.friction};
   const Mat mb{mc.inv_mass, 0.0003f, mc.restitution, mc.friction};  // Walker.cs:168
   const float dt = P.dt_sub;
   const float adx = 0.0f * dt, ady = 980.0f * dt;
-  const uint32_t gid = (uint32_t)(P.env_offset + e);
   uint32_t t = A.rng_t[e];
   uint32_t fault = 0;
-#ifdef WK_REGION_PROF
-  __shared__ WaveProf wprof[SIDE_BLOCK / 64];
-  RegionProf rpv{&wprof[threadIdx.x >> 6]};
-  if ((threadIdx.x & 63) == 0) {
-    for (int r = 0; r < RP_N; r++) { rpv.w->acc[r] = 0; rpv.w->lanes[r] = 0; rpv.w->cnt[r] = 0; }
-    rpv.w->t = __builtin_amdgcn_s_memtime();
-  }
-  RegionProf* rp = &rpv;
-#else
-  RegionProf* rp = nullptr;
-#endif
+  RP_KERNEL_BEGIN(SIDE_BLOCK / 64);  // (probe builds only, wk_region_prof.h)
 
 #pragma unroll 1
   for (int k = 0; k < A.k_steps; k++) {
@@ -1693,22 +1247,11 @@ void k_env_side(EnvParams P, StepArgs A) {
     rp_mark(rp, RP_OTHER);
     // every LDS address of the env-step derived from the thread index afresh (an opaque copy
     // made inside the loop): hoisted out of the loop they were ten loop-invariant VGPRs that
-    // the register allocator kept in scratch (WK_OPQ_LOOP=0: the hoisted form)
-#if WK_OPQ_LOOP
+    // the register allocator kept in scratch
     const int tx = (int)lane_opaque(threadIdx.x);
-#else
-    const int tx = threadIdx.x;
-#endif
     float4* const frec = face_lds + (FS ? tx : 0);
-    float4* const stash = POOL ? pool_lds + (pool::STASH + tx) : frec;
-    float* const wave_pol = (POOL ? (float*)(pool_lds + pool::POL) : pol_lds) + (POLICY ? (tx >> 6) * 768 : 0);
-    if constexpr (POOL) {
-      // which floor slots the block's walkers take this env-step (the list order changes only
-      // at a reset); also the barrier that keeps the policy's stash / tiles from the last
-      // substep's late result reads
-      pc.blk_post = __syncthreads_or(s.post ? 1 : 0) != 0;
-      pc.blk_ep0 = __syncthreads_or(s.post ? 0 : 1) != 0;
-    }
+    float4* const stash = frec;
+    float* const wave_pol = pol_lds + (POLICY ? (tx >> 6) * 768 : 0);
     if (POLICY) {
       get_obs_side(s, side, obs);
       // The policy's matrix-core section needs the most registers of the loop, while the legs'
@@ -1716,7 +1259,7 @@ void k_env_side(EnvParams P, StepArgs A) {
       // face column (free outside the contact clipping) rather than leave them to the spill; the
       // empty asm with a memory clobber keeps the compiler from forwarding the parked values in
       // registers across the section.  Pure data movement: bit-identical.
-      if constexpr (SS != 0 && WK_POLICY_STASH) {
+      if constexpr (SS != 0) {
         park_legs<SS>(s, stash);
         asm volatile("" ::: "memory");
       } else if constexpr (RS != 0) {
@@ -1729,37 +1272,27 @@ void k_env_side(EnvParams P, StepArgs A) {
       for (int d = 0; d < 4; d++) mean[d] = tanhf(z3[d]);
       // (the walker's Philox counter word through an opaque copy: the first round's per-lane
       // products are recomputed per env-step rather than hoisted into seven spilled VGPRs)
-      sample_actions(P, A.lp_const, WK_OPQ_LOOP ? (uint32_t)P.env_offset + lane_opaque((uint32_t)e) : gid, t, mean, a, lp);
-#ifndef WK_PROBE_SLOTROWS
-#define WK_PROBE_SLOTROWS 0  // probe builds only: trajectory rows at the lane slot, not the walker id
-#endif
-#ifndef WK_PROBE_SKIP
-#define WK_PROBE_SKIP 0  // traffic probe builds only: 1 skips the s rows, 2 the done bytes, 4 a / lp / v / r
-#endif
-      if (RECORD && leader) {  // the rows: 16-byte stores (st_row: plain, see WK_TRAJ_NT)
+      sample_actions(P, A.lp_const, (uint32_t)P.env_offset + lane_opaque((uint32_t)e), t, mean, a, lp);
+      if (RECORD && leader) {  // the rows: 16-byte plain stores (st_row)
         // row base (uniform, SGPRs) + the lane's 32-bit offset (global_store saddr form): no
         // per-lane 64-bit pointer per array stays live across the env-step loop (they spilled)
         const size_t row = (size_t)(A.t0 + k) * n;
-        const uint32_t eo = lane_opaque((uint32_t)(WK_PROBE_SLOTROWS ? slot : e));
+        const uint32_t eo = lane_opaque((uint32_t)e);
 #pragma unroll
         for (int q = 0; q < 3; q++)
-          if (!(WK_PROBE_SKIP & 1))
-            st_row4(A.traj_s + row * 12 + (eo * 12u + 4u * q), obs[4 * q], obs[4 * q + 1], obs[4 * q + 2],
-                   obs[4 * q + 3]);
-        if (!(WK_PROBE_SKIP & 4)) {
-          st_row4(A.traj_a + row * 4 + eo * 4u, a[0], a[1], a[2], a[3]);
-          st_row4(A.traj_lp + row * 4 + eo * 4u, lp[0], lp[1], lp[2], lp[3]);
-          st_row(v, A.traj_v + row + eo);
-        }
+          st_row4(A.traj_s + row * 12 + (eo * 12u + 4u * q), obs[4 * q], obs[4 * q + 1], obs[4 * q + 2],
+                  obs[4 * q + 3]);
+        st_row4(A.traj_a + row * 4 + eo * 4u, a[0], a[1], a[2], a[3]);
+        st_row4(A.traj_lp + row * 4 + eo * 4u, lp[0], lp[1], lp[2], lp[3]);
+        st_row(v, A.traj_v + row + eo);
       }
-      if constexpr (SS != 0 && WK_POLICY_STASH) {
+      if constexpr (SS != 0) {
         asm volatile("" ::: "memory");
         unpark_legs<SS>(s, stash);
       } else if constexpr (RS != 0) {
         asm volatile("" ::: "memory");
         unpark_legs<RS, 4>(s, rstash_lds + tx);
       }
-      if constexpr (POOL) __syncthreads();  // stash and tiles read before the queues reuse them
     } else {
 #pragma unroll
       for (int d = 0; d < 4; d++) a[d] = A.actions[((size_t)k * n + e) * 4 + d];
@@ -1774,12 +1307,8 @@ void k_env_side(EnvParams P, StepArgs A) {
     }
 #pragma unroll 1
     for (int it = 0; it < P.iterations; it++) {
-      if constexpr (POOL) {
-        substep_pool<WK_POOL>(s, mp, mb, dt, adx, ady, side, pc, rp);
-      } else {
-        PairTraceDev* tr = (TRACE && active && half == 0) ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
-        substep_side<TRACE, Q, ROUGH, WPB, FS>(s, mp, mb, dt, adx, ady, tr, side, half, rp, ter, frec);
-      }
+      PairTraceDev* tr = (TRACE && active && half == 0) ? A.trace + ((size_t)e * P.iterations + it) : nullptr;
+      substep_side<TRACE, Q, ROUGH, WPB, FS>(s, mp, mb, dt, adx, ady, tr, side, half, rp, ter, frec);
     }
     // Walker.Update + terminal flags (both upper legs and the torso)
     s.prevx = s.posx; s.prevy = s.posy;
@@ -1802,7 +1331,7 @@ void k_env_side(EnvParams P, StepArgs A) {
     }
     if (!side_finite(s)) fault |= 1u;
     const size_t krow = (size_t)k * n;  // (uniform) + the lane's 32-bit offset, as above
-    const uint32_t eo = lane_opaque((uint32_t)(WK_PROBE_SLOTROWS ? slot : e));
+    const uint32_t eo = lane_opaque((uint32_t)e);
     if (A.pos_out && leader) {
       A.pos_out[krow * 2 + eo * 2u] = s.posx;
       A.pos_out[krow * 2 + (eo * 2u + 1u)] = s.posy;
@@ -1811,7 +1340,7 @@ void k_env_side(EnvParams P, StepArgs A) {
       int ep = s.episodes + 1;
       // (the start offset re-read here: a loop-invariant dx or the template's vertices from it
       // would otherwise stay live, i.e. in scratch, across the whole loop)
-      make_template_side(s, WK_OPQ_LOOP ? A.dxoff[lane_opaque((uint32_t)e)] : dx);
+      make_template_side(s, A.dxoff[lane_opaque((uint32_t)e)]);
       s.post = true;
       s.episodes = ep;
     }
@@ -1827,22 +1356,15 @@ void k_env_side(EnvParams P, StepArgs A) {
       if (A.done_out) A.done_out[krow + eo] = terminal ? 1 : 0;
       if (RECORD) {
         const size_t row = (size_t)(A.t0 + k) * n;
-        if (!(WK_PROBE_SKIP & 4)) st_row(reward, A.traj_r + row + eo);
-        if (!(WK_PROBE_SKIP & 2)) st_row((uint8_t)(terminal ? 1 : 0), A.traj_d + row + eo);
+        st_row(reward, A.traj_r + row + eo);
+        st_row((uint8_t)(terminal ? 1 : 0), A.traj_d + row + eo);
       }
     }
     t++;
   }
   // (the side and its record offsets formed here again: kept from the loads they stayed in scratch)
   if (active && half == 0) store_side(s, A.st, lane_opaque((uint32_t)e), (int)(lane_opaque(threadIdx.x) & 1u));
-#ifdef WK_REGION_PROF
-  if ((threadIdx.x & 63) == 0)
-    for (int r = 0; r < RP_N; r++) {
-      atomicAdd(&g_region_prof[r], rpv.w->acc[r]);
-      atomicAdd(&g_region_prof[RP_N + r], rpv.w->lanes[r]);
-      atomicAdd(&g_region_prof[2 * RP_N + r], (unsigned long long)rpv.w->cnt[r]);
-    }
-#endif
+  RP_KERNEL_END();
   fault |= (uint32_t)pswap((float)fault);
   if (leader) {
     const uint32_t eo = lane_opaque((uint32_t)e);  // (addresses formed here, not kept from the loads)
@@ -2044,16 +1566,6 @@ hipError_t launch_env_step(int mode, const EnvParams& P, const StepArgs& A, hipS
   return hipGetLastError();
 }
 #endif  // WK_PART(3)
-#if defined(WK_REGION_PROF) && WK_PART(1)
-extern "C" int wk_region_prof(unsigned long long* out, int reset) {  // out[3 * RP_N]
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_region_prof), sizeof(unsigned long long) * 3 * RP_N) != hipSuccess) return -1;
-  if (reset) {
-    unsigned long long z[3 * RP_N] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_region_prof), z, sizeof(z)) != hipSuccess) return -1;
-  }
-  return 0;
-}
-#endif
 #if WK_PART(3)
 hipError_t launch_env_init(const EnvParams& P, float* st, const float* dx, const uint8_t* mask,
                            int post, hipStream_t s) {
@@ -2080,3 +1592,6 @@ hipError_t launch_returns(int n, int T, int use_gae, float gamma, float lambda, 
 }
 #endif  // WK_PART(3)
 }  // namespace wk
+#if WK_PART(1)
+RP_HOST_READER  // (probe builds only)
+#endif

@@ -456,9 +456,19 @@ hipError_t launch_grad_reduce_adam(const float* partial, int nblocks, float* par
 // number before the abort overwrote it (a wait that ended within the same few microseconds), or
 // blocks of one rank that straddle the timeout, leave the replicas' W / m / v differing -- after
 // WK_ERR_COMM the job must stop or reload a checkpoint on every rank.
+// Timing (x.stamps, wk_comm_xch_profile): thread 0 reads the constant clock at entry, after its
+// flag store, after the block's wait and after the block's last Adam store, and writes the four
+// values with vector stores to the launch's ring slot -- wait time versus own work per minibatch.
 __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
   __shared__ float4 gs[RG][QB];
   __shared__ int live;  // no exchange has timed out (entry), and this block's wait completed
+  uint64_t ts[XCH_POINTS] = {0, 0, 0, 0};
+  const bool stamp = x.stamps != nullptr && threadIdx.x == 0;
+  if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
+  auto flush = [&]() {
+    if (stamp)
+      for (int k = 0; k < XCH_POINTS; k++) x.stamps[blockIdx.x * XCH_POINTS + k] = ts[k];
+  };
   if (threadIdx.x == 0)
     live = __hip_atomic_load(x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u ? 1 : 0;
   const int qi = threadIdx.x % QB, gi = threadIdx.x / QB;
@@ -489,6 +499,7 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
   if (!live) {  // an earlier exchange failed (block-uniform: read after the barrier)
     if (t == 0)
       __hip_atomic_store(x.flag[x.rank] + blockIdx.x, XCH_ABORT, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    flush();
     return;
   }
   const int buf = (int)(x.seq & 1u);
@@ -511,6 +522,7 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
   __syncthreads();
   if (t == 0)
     __hip_atomic_store(x.flag[x.rank] + blockIdx.x, x.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (stamp) ts[1] = __builtin_amdgcn_s_memrealtime();
   if (t < x.nranks && t != x.rank) {
     const uint64_t* f = x.flag[t] + blockIdx.x;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -525,9 +537,11 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
     }
   }
   __syncthreads();
+  if (stamp) ts[2] = __builtin_amdgcn_s_memrealtime();
   if (!live) {  // no grad_out, no Adam; a late peer reading this flag fails this minibatch too
     if (t == 0)
       __hip_atomic_store(x.flag[x.rank] + blockIdx.x, XCH_ABORT, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    flush();
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale peer lines
@@ -540,7 +554,14 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
   }
   if (blockIdx.x == 0 && t == 0 && x.a.W != nullptr)
     __hip_atomic_store(x.err + 1, x.t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (x.stamps != nullptr) {  // (block-uniform) the exit stamp after every thread's stores issued
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
+    flush();
+  }
 }
+int xch_blocks() { return (SLAB / 4 + QB - 1) / QB; }
 size_t xch_region_bytes() { return sizeof(float) * 2 * SLAB + sizeof(uint64_t) * XCH_FLAGS; }
 hipError_t launch_reduce_xch_adam(const XchArgs& x, hipStream_t s) {
   static_assert((SLAB / 4 + QB - 1) / QB <= XCH_FLAGS, "one flag per block");

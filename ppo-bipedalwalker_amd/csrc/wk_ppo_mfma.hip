@@ -31,7 +31,6 @@
 #include "wk_common.h"
 #include "wk_kernels.h"
 #include "wk_mfma_layout.h"
-#include "wk_tail.h"
 
 namespace wk {
 
@@ -88,35 +87,15 @@ DEV float row_sum16(float v) {
 // Block slabs of the ordered reduction, written through to memory (sc1 buffer stores): the
 // kernel-end release then has no dirty slab lines to write back out of the L2, and the
 // reduction reads them from other XCDs anyway (tile-parallel kernel 12.9 -> 12.2 us per launch
-// at 8,192 samples, the reduction unchanged).  -DWK_SLAB_SC1=0: plain stores.
-#ifndef WK_SLAB_SC1
-#define WK_SLAB_SC1 1
-#endif
+// at 8,192 samples, the reduction unchanged).
 struct SlabOut {
   __amdgpu_buffer_rsrc_t r;
-  f4* p;
-  DEV explicit SlabOut(float* base)
-      : r(__builtin_amdgcn_make_buffer_rsrc(base, 0, SLAB * 4, 0x00020000)), p((f4*)base) {}
+  DEV explicit SlabOut(float* base) : r(__builtin_amdgcn_make_buffer_rsrc(base, 0, SLAB * 4, 0x00020000)) {}
   DEV void put(int i, f4 v) const {  // 16-byte element i
-#if WK_SLAB_SC1
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, i * 16, 0, 16);
-#else
-    p[i] = v;
-#endif
   }
 };
-
-// Optional phase profile (build with -DWK_GRAD_PROF; scripts/grad_prof.py): wave 0 of each block
-// accumulates s_memtime deltas per phase, summed over blocks into g_grad_prof.
-#ifdef WK_GRAD_PROF
-__device__ unsigned long long g_grad_prof[16];
-#define GP_MARK(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); gp[k] += t_ - gp_t; gp_t = t_; } while (0)
-#define GP_FLUSH() do { if (tid == 0) for (int k_ = 0; k_ < 12; k_++) atomicAdd(&g_grad_prof[k_], (unsigned long long)gp[k_]); } while (0)
-#else
-#define GP_MARK(k) do {} while (0)
-#define GP_FLUSH() do {} while (0)
-#endif
 
 __global__ __launch_bounds__(64 * mf::WAVES) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_ppo_grad_mfma(GradArgs ga) {
@@ -124,15 +103,8 @@ void k_ppo_grad_mfma(GradArgs ga) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, g = lane >> 4;
-#ifdef WK_GRAD_PROF
-  uint64_t gp[12] = {}, gp_t = __builtin_amdgcn_s_memtime();
-#endif
 
-#ifdef WK_GRAD_NOLOOP  // probe: the launch without its chunk loop (fixed-cost measurement)
-  const int nchunks = 0;
-#else
   const int nchunks = (ga.samples + 15) / 16;
-#endif
   const int nw = gridDim.x * WAVES;
   // gather (CreateBatches, PPOAgent.cs:512-533), one chunk ahead of the math
   struct Smp { f4 sv; float act, lpo, ret, adv; };
@@ -156,7 +128,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
   // ---- stage the weight image (already in operand order, wk_mfma_layout.h): every
   // thread's loads are issued before its first LDS write, so the copy costs one L2
   // round trip instead of one per 4 KB ----
-#ifndef WK_GRAD_NOSTAGE  // probe: no weight staging (fixed-cost measurement)
   {
     constexpr int NV = WEND / 4, PER = (NV + 64 * WAVES - 1) / (64 * WAVES);
     f4 wv[PER];
@@ -171,7 +142,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
       if (e < NV) ((f4*)lds)[e] = wv[i];
     }
   }
-#endif
   float* cb = lds + WEND + wave * CHUNK;
   for (int e = lane; e < 256; e += 64) cb[C_G3 + e] = 0.0f;
   __syncthreads();
@@ -211,7 +181,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
 #pragma unroll
     for (int d = 0; d < 4; d++) w3[d][Mt] = *(const f4*)(lds + W3 + d * 64 + 16 * Mt + 4 * g);
   }
-  GP_MARK(0);  // prologue
 #pragma unroll 1
   for (; c < nchunks; c += nw) {
     const Smp cur = nxt;
@@ -225,12 +194,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
     }
     wave_sync();
 
-    GP_MARK(1);  // gather issue + SX tile
-#ifdef WK_PROBE_EMPTY  // probe: the loop body reduced to the gather and a token accumulation
-    db3 += cb[C_SX + sx(n, g)] + act + lpo + ret + adv;
-    (void)valid;
-    continue;
-#endif
     // ---- layer 1, actor and critic ----
     float sB[3];
 #pragma unroll
@@ -259,7 +222,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
       *(f4*)(cb + C_H1 + tw(n, 16 * Mt + 4 * g)) = h1[Mt];
       *(f4*)(cb + C_HC1 + tw(n, 16 * Mt + 4 * g)) = hc1[Mt];
     }
-    GP_MARK(2);  // layer 1
     // ---- layer 2 (B operand = layer 1's D registers) ----
     f4 w2[4][4];
 #pragma unroll
@@ -285,7 +247,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
       }
       *(f4*)(cb + C_H2 + tw(n, 16 * Mt + 4 * g)) = h2[Mt];
     }
-    GP_MARK(3);  // layer 2
     // ---- output rows: actor z3[0..3] on h2, critic V on hc1 ----
     float p3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, pv = 0.0f;
 #pragma unroll
@@ -307,20 +268,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
     const float z3 = (g == 0 ? p3[0] : g == 1 ? p3[1] : g == 2 ? p3[2] : p3[3]) + b3g;
     const float V = pv + bc2;
 
-    GP_MARK(4);  // output rows
-#ifdef WK_PROBE_NOLOSS
-    const bool use = valid;
-    float criticLoss = use ? (V - ret) * 1e-3f : 0.0f;
-    float actorLoss = use ? (z3 - act) * 1e-3f : 0.0f;
-    const float gz3 = actorLoss;
-    float al[4], q[4];
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-      al[d] = __shfl(actorLoss, n + 16 * d);
-      q[d] = __shfl(gz3, n + 16 * d);
-    }
-    (void)lpo; (void)adv;
-#else
     // ---- PPO derivative for action dimension d = g (PPOAgent.cs:234-326) ----
     const float mean = tanhf(z3);
     float criticLoss = 2.0f * (V - ret);
@@ -355,7 +302,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
       al[d] = __shfl(actorLoss, n + 16 * d);
       q[d] = __shfl(gz3, n + 16 * d);
     }
-#endif
     if (g == 0) {
       diagC += criticLoss;
       diagA += use ? ((((0.0f + al[0]) + al[1]) + al[2]) + al[3]) / 4.0f : 0.0f;
@@ -365,7 +311,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
     }
     db3 += gz3;
     cb[C_G3 + sx(n, g)] = gz3;
-    GP_MARK(5);  // loss
     // ---- gh2 = W3^T gz3 -> gz2; critic gzc1 = (Wc2 dV) * lrelu'(zc1) ----
     f4 gz2[4], gzc1[4];
 #pragma unroll
@@ -383,11 +328,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
       *(f4*)(cb + C_G2 + tw(n, 16 * Mt + 4 * g)) = gz2[Mt];
     }
     wave_sync();
-    GP_MARK(6);  // gz2 / gzc1 + G2 tile
     // ---- dW3 | dWc2 += [gz3; dV]^T [H2 | Hc1]; dW2 += gz2^T H1 (samples on K) ----
-#ifdef WK_PROBE_NOBWD
-    if (ga.samples < 0)
-#endif
     {
       float av[4], bv[4][8], ag[4][4], bh[4][4];
 #pragma unroll
@@ -416,11 +357,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
       }
     }
     wave_sync();  // H2 / Hc1 reads done before G1 / Gc1 overwrite them
-    GP_MARK(7);  // dW3 / dW2
     // ---- gh1^T = W2^T gz2^T (B = gz2 registers) -> gz1 ----
-#ifdef WK_PROBE_NOBWD
-    if (ga.samples < 0)
-#endif
     {
 #pragma unroll
     for (int Mk = 0; Mk < 4; Mk++)
@@ -445,11 +382,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
     }
     }
     wave_sync();
-    GP_MARK(8);  // gh1 + gz1
     // ---- dW1 | db1, dWc1 | dbc1 += gz1^T [S | 1] ----
-#ifdef WK_PROBE_NOBWD
-    if (ga.samples < 0)
-#endif
     {
       float bx[4], a1v[4][4], a1cv[4][4];
 #pragma unroll
@@ -471,13 +404,8 @@ void k_ppo_grad_mfma(GradArgs ga) {
         }
     }
     wave_sync();  // the next chunk rewrites every tile
-    GP_MARK(9);  // dW1
   }
 
-#ifdef WK_GRAD_NOEPI  // probe: no epilogue
-  if (ga.samples >= 0) return;
-#endif
-  GP_MARK(10);  // (loop exit)
   // ---- per-lane sums over the 16 sample lanes of each row ----
 #pragma unroll
   for (int i = 0; i < 16; i++) db2[i] = row_sum16(db2[i]);
@@ -529,9 +457,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
     }
   }
   __syncthreads();
-#ifdef WK_GRAD_NOFOLD  // probe: no block fold
-  if (ga.samples >= 0) return;
-#endif
   // the block fold, 16 bytes per lane and step with every LDS read of a lane issued up front
   // (same element order: ((0 + w0) + w1) + w2) + w3)
   f4* out = (f4*)(ga.partial + (size_t)blockIdx.x * SLAB);
@@ -551,8 +476,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
     for (int w = 0; w < WAVES; w++) acc = acc + sv[k][w];
     if (i < NV) out[i] = acc;
   }
-  GP_MARK(11);
-  GP_FLUSH();
 }
 
 // ---------------------------------------------------------------------------------------
@@ -575,9 +498,6 @@ void k_ppo_grad_mfma(GradArgs ga) {
 // bank-conflict-free; the sample contractions take K step r = samples 4 g + r.  A pair's
 // producer and consumer own disjoint parameters, so they write one slab and the block folds
 // the four pair slabs in pair order (ordered reduction as before).
-#ifndef WK_GRAD_PRIO
-#define WK_GRAD_PRIO 2
-#endif
 namespace ws {
 enum : int {
   RT = 68, T68 = 16 * RT, RSX = 20, TSX = 16 * RSX,
@@ -629,11 +549,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
   }
   pair = __builtin_amdgcn_readfirstlane(pair);
   producer = __builtin_amdgcn_readfirstlane(producer ? 1 : 0) != 0;
-#ifdef WK_GRAD_NOLOOP  // probe: the launch without its chunk loop (fixed-cost measurement)
-  const int nchunks = 0;
-#else
   const int nchunks = (ga.samples + 15) / 16;
-#endif
   const int nw = gridDim.x * PAIRS;
   const int c0 = blockIdx.x * PAIRS + pair;
   const int kp = c0 < nchunks ? (nchunks - 1 - c0) / nw + 1 : 0;         // this pair's chunks
@@ -659,7 +575,6 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
   };
   Smp nxt;
   if (producer) nxt = gather(c0 < nchunks ? c0 : 0);  // in flight while the weights are staged
-#ifndef WK_GRAD_NOSTAGE  // probe: no weight staging (fixed-cost measurement)
   {
     constexpr int NV = WEND / 4, PER = (NV + 512 - 1) / 512;
     f4 wv[PER];
@@ -674,7 +589,6 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
       if (e < NV) ((f4*)lds)[e] = wv[i];
     }
   }
-#endif
   __syncthreads();
   float* const pt = lds + WEND + pair * 2 * TB;  // this pair's two tile buffers
   const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -684,9 +598,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
     // ---------------- producer ----------------
     // (the producer's dependent chain sets the pace: the SIMD's arbiter serves it first, the
     // consumer's independent MFMAs fill the gaps)
-#if WK_GRAD_PRIO
-    __builtin_amdgcn_s_setprio(WK_GRAD_PRIO);
-#endif
+    __builtin_amdgcn_s_setprio(2);
     f4 aw3[4][4], awc2[4], db2[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -706,9 +618,6 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
       }
 #pragma unroll 1
     for (int i = 0; i <= kmax; i++) {
-#ifdef WK_WS_NOPROD  // probe: the consumer alone (on whatever the tiles hold)
-      if (ga.samples < 0)
-#endif
       if (i < kp) {
         const int c = c0 + i * nw;
         float* const tb = pt + (i & 1) * TB;
@@ -854,9 +763,6 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
       }
       __syncthreads();  // chunk i's tiles to the consumer; its reads of buffer (i - 1) & 1 done
     }
-#ifdef WK_GRAD_NOEPI  // probe: no epilogue
-    if (ga.samples >= 0) return;
-#endif
     __syncthreads();  // every wave is done with the weights and tiles
     // ---- the producer's per-lane partials, raw, to R[pair][v][lane]: the whole block forms
     // their sums over the 16 sample lanes of each row below (v order: db2, dWc2, dW3 by
@@ -886,9 +792,6 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
     }
 #pragma unroll 1
     for (int i = 0; i <= kmax; i++) {
-#ifdef WK_WS_NOCONS  // probe: the producer alone
-      if (ga.samples < 0)
-#endif
       if (i >= 1 && i <= kp) {
         float* const tb = pt + ((i - 1) & 1) * TB;
         // gz2 and h1 in N layout (the producer's own registers, read back)
@@ -963,9 +866,6 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
       }
       __syncthreads();
     }
-#ifdef WK_GRAD_NOEPI
-    if (ga.samples >= 0) return;
-#endif
     __syncthreads();  // (matches the producer's: weights and tiles are free)
   }
   __syncthreads();  // the producers' partials are in R
@@ -1034,12 +934,8 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
     f4 acc = z4;
 #pragma unroll
     for (int w = 0; w < PAIRS; w++) acc = acc + sv[k][w];
-#ifdef WK_GRAD_NOWRITE  // probe: no slab write (fixed-cost measurement)
-    if (ga.samples < 0)
-#endif
     if (i < NV) out.put(i, acc);
   }
-  if (ga.tail.on) grad_tail<64 * 2 * PAIRS>(ga.tail, ga.partial, (int)gridDim.x, (float4*)lds);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1085,19 +981,12 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int team = wv >> 2, w = wv & 3;
   const int n = lane & 15, g = lane >> 4;
-#ifdef WK_GRAD_NOLOOP  // probe: the launch without its chunk loop (fixed-cost measurement)
-  const int nchunks = 0;
-#else
   const int nchunks = (ga.samples + 15) / 16;
-#endif
   const int nt = gridDim.x * TEAMS;
   const int c0 = blockIdx.x * TEAMS + team;
   const int kp = c0 < nchunks ? (nchunks - 1 - c0) / nt + 1 : 0;  // this team's chunks
   const int kmax = blockIdx.x * TEAMS < nchunks ? (nchunks - 1 - blockIdx.x * TEAMS) / nt + 1 : 0;
   const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
-#ifdef WK_GRAD_PROF
-  uint64_t gp[12] = {}, gp_t = __builtin_amdgcn_s_memtime();
-#endif
 
   // gather (CreateBatches, PPOAgent.cs:512-533): lane (n, g) holds features g, 4 + g, 8 + g of
   // sample n (layer 1's B operand) and the sample's action dim g entries
@@ -1146,7 +1035,6 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
       *(f4*)(tt + b * TB + O_SX + n * RSX + 12) = f4{1.0f, 0.0f, 0.0f, 0.0f};
   }
 
-  GP_MARK(0);  // prologue: weights issued, first gather issued
   f4 a2[4], aw3[4], a1 = z4, a1c = z4, awc2 = z4, db2 = z4;
 #pragma unroll
   for (int i = 0; i < 4; i++) { a2[i] = z4; aw3[i] = z4; }
@@ -1180,9 +1068,7 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
       }
       *(f4*)(tb + O_H1 + n * RT + 16 * w + 4 * g) = h1;
     }
-    GP_MARK(1);  // layer 1
     __syncthreads();  // B1: the team's H1 tile
-    GP_MARK(2);
     f4 h2 = z4;
     if (live) {
       // ---- layer 2 of tile w (k order (Mp, r), as k_ppo_grad_ws) ----
@@ -1215,9 +1101,7 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
       tb[O_P + w * RP + g * 16 + n] = g == 0 ? p3[0] : g == 1 ? p3[1] : g == 2 ? p3[2] : p3[3];
       if (g == 0) tb[O_P + w * RP + 64 + n] = pv;
     }
-    GP_MARK(3);  // layer 2 + rows
     __syncthreads();  // B2: the team's partial dots
-    GP_MARK(4);
     if (live) {
       float z3 = 0.0f, pv = 0.0f;
 #pragma unroll
@@ -1288,9 +1172,7 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
       *(f4*)(tb + O_G2 + n * RT + 16 * w + 4 * g) = gz2;
       *(f4*)(tb + O_GC1 + n * RT + 16 * w + 4 * g) = gzc1;
     }
-    GP_MARK(5);  // loss + VALU gradients
     __syncthreads();  // B3: the team's G2 tile
-    GP_MARK(6);
     if (live) {
       // ---- dW2[tile w][:] += gz2^T H1 (samples on K: step r = samples 4 g + r) ----
       {
@@ -1334,7 +1216,6 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
         a1c = mfma(acv[r], bx[r], a1c);
       }
     }
-    GP_MARK(7);  // backward
   }
 
   // ---- totals over the 16 sample lanes of each row, then this wave's part of the slab ----
@@ -1350,7 +1231,6 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
   diagC = row_sum16(diagC);
   diagA = row_sum16(diagA);
   skipped = row_sum16(skipped);
-  GP_MARK(8);  // row sums
   // each team's slab in LDS in parameter order (every entry written by exactly one wave of
   // the team), then the block writes (t0 [+ t1]) with 16-byte coalesced stores
   __syncthreads();  // every wave is done with the tiles
@@ -1403,9 +1283,6 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
       if (i < NV) out.put(i, acc);
     }
   }
-  GP_MARK(9);  // slab
-  GP_FLUSH();
-  if (ga.tail.on) grad_tail<256 * TEAMS>(ga.tail, ga.partial, (int)gridDim.x, (float4*)lds);
 }
 
 // the weight image from the flat parameters (initialisation, wk_set_weights)
@@ -1415,16 +1292,6 @@ __global__ void k_swizzle(const float* __restrict__ W, float* __restrict__ Wz) {
 }
 
 int mfma_image_floats() { return mf::WEND; }
-#ifdef WK_GRAD_PROF
-extern "C" int wk_grad_prof(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_grad_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
-  if (reset) {
-    unsigned long long z[16] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_grad_prof), z, sizeof(z)) != hipSuccess) return -1;
-  }
-  return 0;
-}
-#endif
 hipError_t launch_swizzle(const float* W, float* Wz, hipStream_t s) {
   hipLaunchKernelGGL(k_swizzle, dim3((NPARAM + 255) / 256), dim3(256), 0, s, W, Wz);
   return hipGetLastError();

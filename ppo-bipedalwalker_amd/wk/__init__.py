@@ -43,7 +43,19 @@ EXPORTS = [
     "wk_profile_get", "wk_profile_reset", "wk_count_events", "wk_snapshot", "wk_time_gradient",
     "wk_time_gradient_ex", "wk_grad_kernel", "wk_rollout_mapping",
     "wk_comm_ipc_handle", "wk_comm_init_ipc", "wk_comm_info", "wk_comm_set_timeout",
+    "wk_comm_xch_profile", "wk_comm_xch_stamps", "wk_check_state", "wk_take_actions",
+    "wk_object_update", "wk_joint_step", "wk_body_order",
 ]
+
+
+def check_state(state):
+    """wk_check_state (host only, no device): (ok, first bad walker, first bad record body)"""
+    import numpy as np
+    st = np.ascontiguousarray(state, dtype=np.float32)
+    be, bb = C.c_int(), C.c_int()
+    lib = load_library()
+    r = lib.wk_check_state(st.ctypes.data, int(st.size // STATE_FLOATS), C.byref(be), C.byref(bb))
+    return r == 0, be.value, bb.value
 
 
 class WkConfig(C.Structure):
@@ -244,6 +256,13 @@ def load_library(path=None):
         "wk_comm_ipc_handle": (I, [P, P]),
         "wk_comm_init_ipc": (I, [P, I, I, P]),
         "wk_comm_set_timeout": (I, [P, C.c_double]),
+        "wk_comm_xch_profile": (I, [P, I]),
+        "wk_check_state": (I, [P, I, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        "wk_take_actions": (I, [P, I, P]),
+        "wk_object_update": (I, [P, I, C.c_float]),
+        "wk_joint_step": (I, [P]),
+        "wk_body_order": (I, [P, I, P, C.POINTER(C.c_int)]),
+        "wk_comm_xch_stamps": (I, [P, P, I, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "wk_profile_enable": (I, [P, I]),
         "wk_profile_get": (I, [P, C.POINTER(Profile)]),
         "wk_profile_reset": (I, [P]),
@@ -725,6 +744,44 @@ class Engine:
         k, f = C.c_int(), C.c_int()
         self._chk(self.lib.wk_comm_info(self.h, C.byref(k), C.byref(f)), "wk_comm_info")
         return self.COMM_KINDS[k.value], bool(f.value & 1)
+
+    # the reference's per-body call shape (Environment.StepObjects, Environment.cs:126-143)
+    def take_actions(self, env, actions):
+        """wk_take_actions: Walker.TakeActions for walker env (the next frame's torques)"""
+        a = _f32(actions).reshape(4).copy()
+        self._chk(self.lib.wk_take_actions(self.h, int(env), _ptr(a)), "wk_take_actions")
+
+    def object_update(self, list_count, delta_time):
+        """wk_object_update: one IObject.Update call; True when this call ran the frame's step"""
+        r = self.lib.wk_object_update(self.h, int(list_count), float(delta_time))
+        self._chk(min(r, 0), "wk_object_update")
+        return r == 1
+
+    def joint_step(self):
+        self._chk(self.lib.wk_joint_step(self.h), "wk_joint_step")
+
+    def body_order(self, env):
+        """wk_body_order: walker env's body list as part ids (floor last in episode 0, first after
+        a reset)"""
+        parts, n = (C.c_int * 15)(), C.c_int()
+        self._chk(self.lib.wk_body_order(self.h, int(env), parts, C.byref(n)), "wk_body_order")
+        return list(parts[: n.value])
+
+    def xch_profile(self, minibatches):
+        """wk_comm_xch_profile: stamp the next exchange launches (a ring of `minibatches`; 0 off)"""
+        self._chk(self.lib.wk_comm_xch_profile(self.h, int(minibatches)), "wk_comm_xch_profile")
+
+    def xch_stamps(self, max_launches=1 << 16):
+        """wk_comm_xch_stamps: uint64 [launches, blocks, 4] constant-clock ticks (10 ns) per block
+        -- entry, slab published, peers' flags seen, exit -- for the last stamped launches"""
+        import numpy as np
+        n, b = C.c_int(), C.c_int()
+        self._chk(self.lib.wk_comm_xch_stamps(self.h, None, 0, C.byref(n), C.byref(b)),
+                  "wk_comm_xch_stamps")
+        buf = np.zeros((max_launches, b.value, 4), np.uint64)
+        self._chk(self.lib.wk_comm_xch_stamps(self.h, buf.ctypes.data, max_launches, C.byref(n),
+                                              C.byref(b)), "wk_comm_xch_stamps")
+        return buf[: n.value]
 
     def allreduce_test(self, x):
         x = _f32(x).copy()

@@ -91,3 +91,39 @@ def test_valu_ceiling_uses_the_launched_grid():
     assert bench.valu_ceiling_of(two)[0] == bench.PEAK_NOFMA
     old = {"lanes_per_walker": 2, "walkers_per_wave": 32, "waves": 2048}  # a pre-round-5 mapping
     assert bench.valu_ceiling_of(old)[0] == bench.PEAK_NOFMA
+
+
+def test_compact_line_falls_back_to_the_contract_keys():
+    """ADVICE r5: when the config / CPU baseline / rehearsal themselves push the line past 4 KB,
+    the line keeps the contract keys and the detail file, and stays under the limit"""
+    full = _full()
+    full["config"]["workload"] = "x" * 5000
+    full["rehearsal"] = "y" * 3000
+    line = bench.compact_line(full, "gpurun_out/bench_detail.json")
+    assert len(line) < 4096, len(line)
+    out = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "detail_file"):
+        assert k in out, k
+    assert out["value"] == full["value"]
+
+
+def test_xch_stamp_summary():
+    """the exchange kernel's per-block stamps (VERDICT r5 #3) -> span / wait / own / gap in us"""
+    import numpy as np
+    st = np.zeros((3, 2, 4), np.uint64)
+    for l in range(3):
+        base = 10000 * l
+        # block 0: entry, published +100 ticks (1 us), peers seen +300 (3 us wait), exit +150
+        st[l, 0] = [base, base + 100, base + 400, base + 550]
+        st[l, 1] = [base + 10, base + 120, base + 420, base + 560]
+    s = bench.xch_stamp_summary(st)
+    assert s["launches"] == 3 and s["blocks"] == 2
+    assert abs(s["span_us_median"] - 5.6) < 1e-9
+    assert abs(s["wait_us_median"] - 3.0) < 1e-9
+    assert abs(s["own_us_median"] - 2.5) < 1e-9  # (1.0 + 1.5, 1.1 + 1.4)
+    assert abs(s["gap_us_median"] - (100.0 - 5.6)) < 1e-9
+    full = _full()
+    full["xch_profile"] = {"per_rank": [s, s]}
+    out = json.loads(bench.compact_line(full))
+    assert out["xch_profile_us"][1]["wait"] == 3.0

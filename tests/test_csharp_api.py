@@ -64,3 +64,22 @@ def test_native_calls_are_declared_imports():
     declared = set(re.findall(r"public static extern \S+ (wk_\w+)\(", NATIVE))
     used = set(re.findall(r"Wk\.(wk_\w+)\(", API))
     assert used and used <= declared, used - declared
+
+
+def test_update_keeps_the_reference_call_shape():
+    """VERDICT r5 #5 / ADVICE r5: Environment.StepObjects (Environment.cs:130-141) calls
+    IObject.Update on every body, every substep; RigidBody.Update must not step the context per
+    call (it forwards to wk_object_update, whose frame's first call steps once -- checked against
+    wk_step on the GPU, tests/test_gpu_call_shape.py); TakeActions stores torques natively and
+    Bodies() returns the list in its current order (floor first after a reset)"""
+    rb = _members("class", "RigidBody")
+    upd = rb[rb.index("public void Update(List<RigidBody> rigidBodies, float deltaTime)"):]
+    upd = upd[:upd.index("\n        }")]
+    assert "wk_object_update(_ctx, rigidBodies.Count, deltaTime)" in upd and "wk_step" not in upd
+    assert "PendingActions" not in API
+    wa = _members("class", "Walker")
+    assert "wk_take_actions(_ctx, Index, actions)" in wa
+    assert "wk_body_order(_ctx, Index, parts, out int n)" in wa
+    assert "List<Joint> GetJoints()" in wa
+    jt = _members("class", "Joint")
+    assert "public void Step() => Wk.wk_joint_step(_ctx);" in jt

@@ -479,26 +479,3 @@ def test_quad_sparse_equals_dense(wk, monkeypatch):
     for key in a:
         np.testing.assert_array_equal(a[key], b[key], err_msg=key)
     np.testing.assert_array_equal(eng.get_state(), dense.get_state())
-
-
-@pytest.mark.parametrize("mode", ["1", "2"])
-def test_fused_minibatch_tail_is_bit_identical(wk, monkeypatch, mode):
-    """the optional fused minibatch tail (WK_GRAD_TAIL=1 release / acquire, 2 sc1 hand-off: the
-    gradient launch's last-arriving blocks run the ordered slab reduction + Adam, wk_tail.h)
-    against the default separate reduction launch: the same association, so the same weights,
-    Adam moments and diagnostics bit for bit, at the three gradient kernels' sizes (tp1 / tp / ws)"""
-    for n, T, M in ((4096, 16, 4096), (8192, 8, 8192), (8192, 8, 65536)):
-        outs = []
-        for tail in ("0", mode):
-            monkeypatch.setenv("WK_GRAD_TAIL", tail)
-            eng = wk.Engine(n, seed=SEED, Horizon=T, RandomizeStart=1, Minibatch=M, Epochs=2)
-            eng.rollout(T)
-            d = eng.ppo_update(update_index=0)
-            outs.append((eng.get_weights(), eng.get_adam(), d, eng.grad_kernel(M)))
-            eng.close()
-        (w0, a0, d0, k0), (w1, a1, d1, k1) = outs
-        assert k0 == k1
-        np.testing.assert_array_equal(w0, w1, err_msg=f"{n} {M} {k0}")
-        for x, y in zip(a0, a1):
-            np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
-        assert d0 == d1
