@@ -429,7 +429,10 @@ int wk_comm_init_host(wk_ctx* ctx, int rank, int nranks, wk_host_allreduce_fn fn
  * marks its flags aborted, so a late peer fails that same minibatch instead of applying it, and
  * wk_get_adam reports the steps actually applied.  The replicas may still differ after a
  * failure (a peer that read this rank's flag just before the abort, or blocks straddling the
- * bound): stop the job or reload a checkpoint on every rank.  wk_minibatch_gradient and
+ * bound), and the failed context stays failed (its error word and aborted flags are not cleared
+ * by wk_checkpoint_load): stop the job, or on every rank destroy the context, create a new one,
+ * map the exchange again (wk_comm_ipc_handle / wk_comm_init_ipc) and load a checkpoint.
+ * wk_minibatch_gradient and
  * wk_train_batch(apply_adam = 0) run the exchange as well (collective calls: every rank must
  * make them), returning the sum over the ranks as on an RCCL context. */
 enum { WK_IPC_HANDLE_BYTES = 128 };

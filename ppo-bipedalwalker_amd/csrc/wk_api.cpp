@@ -1288,8 +1288,9 @@ static int xch_status(wk_ctx* c) {
   if (err[0]) {
     c->adam_t = (int)err[1];
     SETERR(c, "IPC gradient exchange: a peer did not publish its minibatch slab within %.1f s or "
-           "gave up on it (no Adam step applied since step %u; the replicas may differ: stop the "
-           "job or reload a checkpoint on every rank)",
+           "gave up on it (no Adam step applied since step %u; the replicas may differ and this "
+           "context stays failed: stop the job, or on every rank destroy the context, create and "
+           "map a new one and load a checkpoint)",
            (double)c->xch_timeout_ticks / wk::XCH_TICKS_PER_S, err[1]);
     return WK_ERR_COMM;
   }

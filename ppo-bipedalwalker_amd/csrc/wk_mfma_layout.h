@@ -23,33 +23,42 @@ enum : int {
 static_assert(WEND % 4 == 0, "16-byte copies");
 }  // namespace mf
 
+// a float store; WT: written through (relaxed agent-scope atomic store = global_store sc1: the
+// line leaves the L2 clean, MI355X_MICROARCH.md), so a later release has nothing of it to write back
+template <bool WT>
+__device__ __forceinline__ void st_f(float* p, float v) {
+  if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
 // write parameter p (value v) to its image position(s)
+template <bool WT = false>
 __device__ inline void mf_scatter_param(float* __restrict__ Wz, int p, float v) {
   using namespace mf;
   if (p < OFF_C_B1 || (p >= OFF_A_W1 && p < OFF_A_B1)) {  // W1 (critic / actor) [64][12]
     const bool critic = p < OFF_C_B1;
     const int q = p - (critic ? OFF_C_W1 : OFF_A_W1);
     const int j = q / 12, k = q % 12;
-    Wz[(critic ? CW1F : AW1F) + ((j >> 4) * 3 + (k >> 2)) * 64 + 16 * (k & 3) + (j & 15)] = v;
+    st_f<WT>(&Wz[(critic ? CW1F : AW1F) + ((j >> 4) * 3 + (k >> 2)) * 64 + 16 * (k & 3) + (j & 15)], v);
   } else if (p < OFF_C_W2) {
-    Wz[BC1 + p - OFF_C_B1] = v;
+    st_f<WT>(&Wz[BC1 + p - OFF_C_B1], v);
   } else if (p < OFF_C_B2) {
-    Wz[WC2 + p - OFF_C_W2] = v;
+    st_f<WT>(&Wz[WC2 + p - OFF_C_W2], v);
   } else if (p < OFF_A_W1) {
-    Wz[BC2] = v;
+    st_f<WT>(&Wz[BC2], v);
   } else if (p < OFF_A_W2) {
-    Wz[BA1 + p - OFF_A_B1] = v;
+    st_f<WT>(&Wz[BA1 + p - OFF_A_B1], v);
   } else if (p < OFF_A_B2) {  // W2 [64 j][64 k], both operand orders
     const int q = p - OFF_A_W2;
     const int j = q >> 6, k = q & 63;
-    Wz[W2F + (((j >> 4) * 4 + (k >> 4)) * 64 + 16 * ((k & 15) >> 2) + (j & 15)) * 4 + (k & 3)] = v;
-    Wz[W2B + (((k >> 4) * 4 + (j >> 4)) * 64 + 16 * ((j & 15) >> 2) + (k & 15)) * 4 + (j & 3)] = v;
+    st_f<WT>(&Wz[W2F + (((j >> 4) * 4 + (k >> 4)) * 64 + 16 * ((k & 15) >> 2) + (j & 15)) * 4 + (k & 3)], v);
+    st_f<WT>(&Wz[W2B + (((k >> 4) * 4 + (j >> 4)) * 64 + 16 * ((j & 15) >> 2) + (k & 15)) * 4 + (j & 3)], v);
   } else if (p < OFF_A_W3) {
-    Wz[BA2 + p - OFF_A_B2] = v;
+    st_f<WT>(&Wz[BA2 + p - OFF_A_B2], v);
   } else if (p < OFF_A_B3) {
-    Wz[W3 + p - OFF_A_W3] = v;
+    st_f<WT>(&Wz[W3 + p - OFF_A_W3], v);
   } else {
-    Wz[BA3 + p - OFF_A_B3] = v;
+    st_f<WT>(&Wz[BA3 + p - OFF_A_B3], v);
   }
 }
 

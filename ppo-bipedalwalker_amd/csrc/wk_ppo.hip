@@ -456,6 +456,15 @@ hipError_t launch_grad_reduce_adam(const float* partial, int nblocks, float* par
 // number before the abort overwrote it (a wait that ended within the same few microseconds), or
 // blocks of one rank that straddle the timeout, leave the replicas' W / m / v differing -- after
 // WK_ERR_COMM the job must stop or reload a checkpoint on every rank.
+// Hand-off (round 6, MI355X_MICROARCH.md's valid forms at system scope): producer -- every wave's
+// slab stores drained (s_waitcnt vmcnt(0)), block barrier, one lane's release store of the flag;
+// consumer -- relaxed polls of the peers' flags by the polling wave, ONE acquire by that wave,
+// s_waitcnt, block barrier, then the peer loads.  Adam's and grad_out's stores are written through
+// (st_f<true>), so the next minibatch's release finds no dirty lines of them to write back.
+// Measured uncontended at the 8-GPU shard's minibatch (scripts/r06_xch_own.py, 2 ranks on one
+// GPU): 19.0 -> 8.2 us per launch (kernel trace), own work 13.9 -> 4.8 us per block (stamps),
+// against 4.9 us for k_grad_reduce_fused<true> on the same slabs; before, every poll was an
+// acquire load and every thread fenced.
 // Timing (x.stamps, wk_comm_xch_profile): thread 0 reads the constant clock at entry, after its
 // flag store, after the block's wait and after the block's last Adam store, and writes the four
 // values with vector stores to the launch's ring slot -- wait time versus own work per minibatch.
@@ -527,7 +536,7 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
     const uint64_t* f = x.flag[t] + blockIdx.x;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t seen;
-    while ((seen = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) < x.seq) {
+    while ((seen = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) < x.seq) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > x.timeout_ticks) break;
       __builtin_amdgcn_s_sleep(2);
     }
@@ -535,6 +544,10 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
       atomicOr(x.err, 1u);
       live = 0;
     }
+  }
+  if (t < 64) {  // ONE acquire (system scope), by the polling wave, before the barrier
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
   if (stamp) ts[2] = __builtin_amdgcn_s_memrealtime();
@@ -544,13 +557,12 @@ __global__ __launch_bounds__(RG * QB) void k_reduce_xch_adam(XchArgs x) {
     flush();
     return;
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale peer lines
   if (gi < 4 && q < SLAB / 4) {
     float sum = x.rank == 0 ? mine : x.slab[0][(size_t)buf * SLAB + p];
     for (int r = 1; r < x.nranks; r++)
       sum = sum + (r == x.rank ? mine : x.slab[r][(size_t)buf * SLAB + p]);
-    x.grad_out[p] = sum;
-    if (adam_lane) adam_apply(x.a, p, sum, m0, v0, w0);
+    st_f<true>(&x.grad_out[p], sum);  // (written through: see below)
+    if (adam_lane) adam_apply<true>(x.a, p, sum, m0, v0, w0);
   }
   if (blockIdx.x == 0 && t == 0 && x.a.W != nullptr)
     __hip_atomic_store(x.err + 1, x.t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

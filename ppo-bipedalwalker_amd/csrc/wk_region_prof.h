@@ -14,8 +14,7 @@
 namespace wk {
 
 enum { RP_JOINT, RP_INTEG, RP_AABB_LL, RP_AABB_LF, RP_AABB_BF, RP_SAT_LL, RP_SAT_LF, RP_SAT_BF,
-       RP_CON_LL, RP_CON_LF, RP_CON_BF, RP_IMP_LL, RP_IMP_LF, RP_IMP_BF, RP_POLICY, RP_OTHER,
-       RP_HELP, RP_N };  // (RP_HELP: the wave-level helper passes)
+       RP_CON_LL, RP_CON_LF, RP_CON_BF, RP_IMP_LL, RP_IMP_LF, RP_IMP_BF, RP_POLICY, RP_OTHER, RP_N };
 #ifdef WK_REGION_PROF
 static __device__ unsigned long long g_region_prof[3 * RP_N];  // ticks, lane sums, counts
 struct WaveProf { unsigned long long acc[RP_N]; unsigned long long lanes[RP_N]; unsigned cnt[RP_N]; unsigned long long t; };

@@ -18,17 +18,19 @@ enum { RG = 16 };
 enum { QB = 16 };  // parameter quads per job (RG x QB threads; 16 timed best of 4 / 8 / 16)
 
 // DenseLayer.Adam (DenseLayer.cs:125-159) for one parameter, from its current m, v, w
+// (WT: the stores written through, see st_f)
+template <bool WT = false>
 __device__ __forceinline__ void adam_apply(const AdamArgs& a, int p, float gr, float m0, float v0, float w0) {
   float m = (gr * a.c1) + (m0 * a.beta1);
   float v = (v0 * a.beta2) + ((gr * gr) * a.c2);
-  a.m[p] = m;
-  a.v[p] = v;
+  st_f<WT>(&a.m[p], m);
+  st_f<WT>(&a.v[p], v);
   float mh = m / a.bc1;
   float vh = v / a.bc2;
   float den = sqrtf(vh) + a.eps;
   const float w = w0 - ((mh / den) * a.alpha);
-  a.W[p] = w;
-  if (a.Wz) mf_scatter_param(a.Wz, p, w);
+  st_f<WT>(&a.W[p], w);
+  if (a.Wz) mf_scatter_param<WT>(a.Wz, p, w);
 }
 
 // One job of the one-launch reduction for nblocks <= RG * RG (thread t of 256: group gi = t / QB,

@@ -18,8 +18,8 @@ L = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 names = ["joint", "integrate", "aabb leg-leg", "aabb leg-floor", "aabb torso-floor", "sat leg-leg",
          "sat leg-floor", "sat torso-floor", "contact leg-leg", "contact leg-floor",
          "contact torso-floor", "move+imp leg-leg", "move+imp leg-floor", "move+imp torso-floor",
-         "policy", "other", "helper passes"]  # (csrc/wk_region_prof.h RP_*; round 5's pool regions
-                                              #  are gone with the pooled stages)
+         "policy", "other"]  # (csrc/wk_region_prof.h RP_*; round 5's pool regions and round 6's
+                             #  helper passes are gone with the code they timed)
 NR = len(names)
 R = int(os.environ.get("REGIME_ITERS", "0"))
 eng = wk.Engine(n, seed=20250905, Horizon=max(T, 64 if R else T), RandomizeStart=1, LanesPerWalker=L)
