@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-5 GPU driver (STEPS="tests smoke bench trace"): every GPU step has its own time limit,
+# Round GPU driver (ROUND=r06 STEPS="tests smoke bench trace pmc"): every GPU step has its own time limit,
 # and a hang / abort / fault (124, 134, 137, 139) or a failure stops the call.
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-R=${ROUND:-r05}
+R=${ROUND:-r06}
 fatal() { case "$1" in 124|134|137|139) echo "FATAL rc=$1 in $2"; exit "$1";; esac; [ "$1" -eq 0 ] || exit "$1"; }
 for s in ${STEPS:-tests smoke bench}; do
   case "$s" in

@@ -105,6 +105,23 @@ def test_ipc_exchange_equals_host_allreduce(two_rank_runs):
         assert float(h["cd"]) == float(i["cd"]) and float(h["ad"]) == float(i["ad"])
 
 
+def test_ipc_exchange_clock_stamps(two_rank_runs):
+    """wk_comm_xch_profile stamps every exchange launch per block -- entry, slab
+    published, every peer's flag seen, exit -- in that order, and the launches follow each other
+    on the stream (the next launch's first entry after this one's last exit: a gradient kernel
+    runs between them); the summary bench.py --xch-profile prints from them is consistent"""
+    import bench
+    for r in two_rank_runs["ipc"]:
+        st = r["stamps"]
+        assert st.shape == (24, 97, 4), st.shape  # 2 updates x 3 epochs x 4 minibatches
+        assert (st > 0).all()
+        d = np.diff(st.astype(np.int64), axis=2)
+        assert (d >= 0).all()  # entry <= published <= peers seen <= exit
+        assert (st[1:, :, 0].min(axis=1) >= st[:-1, :, 3].max(axis=1)).all()
+        s = bench.xch_stamp_summary(st)
+        assert s["launches"] == 24 and 0 < s["own_us_median"] < s["span_us_median"] + 1e-9
+
+
 def test_three_ranks_ipc_rank_order_sum(tmp_path):
     """three processes (an odd rank count): the IPC exchange sums the ranks' local slabs in rank
     order, ((g0 + g1) + g2) in float32, and every replica applies the same Adam step"""

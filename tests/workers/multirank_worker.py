@@ -141,14 +141,17 @@ eng.rollout(T)  # a second iteration: the replicas stay identical
 eng.ppo_update(update_index=1)
 w2 = eng.get_weights()
 # several minibatches and epochs per update (the exchange's sequence numbers and double
-# buffering): 3 epochs x 4 minibatches, twice
+# buffering): 3 epochs x 4 minibatches, twice -- on the IPC exchange with the clock stamps on
+if mode == "ipc":
+    eng.xch_profile(32)
 for u in (2, 3):
     eng.rollout(T)
     eng.ppo_update(epochs=3, minibatch=shard.minibatch_local // 4,
                    minibatch_global=shard.minibatch_global // 4, update_index=u)
 w3 = eng.get_weights()
 m3, v3, t3 = eng.get_adam()
-np.savez(os.path.join(out_dir, f"rank{rank}.npz"), w0=w0, w1=w1, m1=m1, v1=v1, t1=t1, w2=w2,
+stamps = eng.xch_stamps(32) if mode == "ipc" else np.zeros((0, 0, 4), np.uint64)
+np.savez(os.path.join(out_dir, f"rank{rank}.npz"), w0=w0, w1=w1, m1=m1, v1=v1, t1=t1, w2=w2, stamps=stamps,
          w3=w3, m3=m3, v3=v3, t3=t3,
          g_local=g_local, g_x=g_x, cd=cd, ad=ad, cd_l=cd_l, ad_l=ad_l, same_traj=same_traj,
          same_state=same_state, state=eng.get_state())
