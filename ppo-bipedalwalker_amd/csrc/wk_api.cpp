@@ -85,6 +85,8 @@ struct wk_ctx {
   unsigned long long* counts = nullptr;  // [WK_NEV] device (wk_count_events)
   int32_t* order = nullptr;       // [n] lane order of the split physics kernels (null: identity)
   uint32_t* order_cnt = nullptr;  // [order_cells(n)] episode-0 walkers per tile + swap count
+  unsigned long long* pace = nullptr;  // [PACE_SLOTS] the pair kernel's per-SIMD progress tags
+  uint32_t pace_seq = 0;
   // comm
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
@@ -414,6 +416,17 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
       ALLOC(x->order_cnt, sizeof(uint32_t) * wk::order_cells((int)n));
     }
   }
+  // the pair kernel's pacing of co-resident waves (k_env_side); test hook WK_PACE=0: without
+  if (P.lanes == 2) {
+    const char* o = getenv("WK_PACE");
+    if (!(o && o[0] == '0')) {
+      ALLOC(x->pace, sizeof(unsigned long long) * wk::PACE_SLOTS);
+      if (hipMemset(x->pace, 0, sizeof(unsigned long long) * wk::PACE_SLOTS) != hipSuccess) {
+        x->err = "pacing table clear failed";
+        return fail(WK_ERR_HIP);
+      }
+    }
+  }
 #undef ALLOC
   // synthetic randomisation of the initial state (BASELINE.json config 2 / 5)
   std::vector<float> dx(n, 0.0f);
@@ -466,7 +479,7 @@ int wk_destroy(wk_ctx* c) {
   void* bufs[] = {c->st, c->dxoff, c->mat, c->rng_t, c->W, c->Wz, c->m, c->v, c->grad, c->ts, c->ta,
                   c->tlp, c->tr, c->tv, c->tret, c->tadv, c->td, c->partial, c->scratch, c->scratch2,
                   c->ep_acc, c->ep_len, c->ep_scratch, c->ep_rowcnt, c->ep_count, c->ep_log,
-                  c->loss_log, c->props, c->snap, c->counts, c->order, c->order_cnt};
+                  c->loss_log, c->props, c->snap, c->counts, c->order, c->order_cnt, c->pace};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -539,6 +552,8 @@ static hipError_t launch_physics(wk_ctx* c, int mode, wk::StepArgs& A) {
     }
     A.order = c->order;
   }
+  A.pace = c->pace;
+  A.pace_seq = ++c->pace_seq;
   return wk::launch_env_step(mode, c->P, A, c->stream);
 }
 

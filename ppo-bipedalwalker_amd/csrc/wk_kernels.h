@@ -60,7 +60,12 @@ struct StepArgs {
   float* props;              // scene props [n][SceneDev::pstride] (k_env_scene) or null
   unsigned long long* counts;  // [NEV] event totals (counting replay, mode 4) or null
   const int32_t* order;      // k_env_side: walker of lane slot s (wk_order.hip) or null (identity)
+  // k_env_side pair mapping: per-SIMD progress tags of its two co-resident waves
+  // ([PACE_SLOTS], zeroed at creation; null: no pacing) and this launch's sequence number
+  unsigned long long* pace;
+  uint32_t pace_seq;
 };
+enum : int { PACE_SLOTS = 8 * 8 * 2 * 16 * 4 };  // XCC x SE x SH x CU x SIMD (HW_ID fields)
 
 // scene props (wk_scene.inc): Square / Triangle / Hexagon bodies after the floor, the same
 // shapes for every walker; per walker and prop k the state x[nv], y[nv], cx, cy, vx, vy, w,

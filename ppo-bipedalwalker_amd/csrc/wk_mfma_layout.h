@@ -31,6 +31,58 @@ __device__ __forceinline__ void st_f(float* p, float v) {
   else *p = v;
 }
 
+// Exchanges between the four 16-lane rows of a wave (lane l = 16 g + n: row g, the MFMA
+// operands' lane group) on gfx950's permlane swaps -- two VALU instructions, no LDS round trip
+// and no lane-index arithmetic as __shfl / __shfl_xor (ds_bpermute_b32) need.  Called with the
+// whole wave active.
+//   v_permlane16_swap(v, v): odd rows of the first copy <-> even rows of the second, so
+//     a = rows [r0 r0 r2 r2], b = rows [r1 r1 r3 r3]
+//   v_permlane32_swap(v, v): upper half of the first <-> lower half of the second, so
+//     lo = halves [lo lo], hi = halves [hi hi]
+__device__ __forceinline__ void rows_pair_swap(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void halves_swap(float v, float& lo, float& hi) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  lo = __uint_as_float(r[0]);
+  hi = __uint_as_float(r[1]);
+}
+// (v + __shfl_xor(v, 16)) then + __shfl_xor(., 32), in every lane: the rows whose own value is
+// the second operand here get the same sum, fp32 addition being commutative
+__device__ __forceinline__ float rows_sum4(float v) {
+  float a, b, lo, hi;
+  rows_pair_swap(v, a, b);
+  halves_swap(a + b, lo, hi);
+  return lo + hi;
+}
+__device__ __forceinline__ float rows_max4(float v) {  // the same with fmaxf
+  float a, b, lo, hi;
+  rows_pair_swap(v, a, b);
+  halves_swap(__builtin_fmaxf(a, b), lo, hi);
+  return __builtin_fmaxf(lo, hi);
+}
+// rows_sum4(p[g]) in lane (n, g) -- the four sums with each lane keeping its own row's, as a
+// reduce-scatter in three swaps: permlane16_swap(p0, p1) gives rows [p0.r0 p1.r0 p0.r2 p1.r2]
+// and [p0.r1 p1.r1 p0.r3 p1.r3] (summed: row g holds p_{g&1} over rows {g&2, (g&2)+1}), the same
+// for p2 / p3, then the halves' swap adds rows {0,1} + {2,3}: the association of rows_sum4
+__device__ __forceinline__ float rows_rsum4(const float p[4]) {
+  const auto u = __builtin_amdgcn_permlane16_swap(__float_as_uint(p[0]), __float_as_uint(p[1]), false, false);
+  const auto w = __builtin_amdgcn_permlane16_swap(__float_as_uint(p[2]), __float_as_uint(p[3]), false, false);
+  const float s01 = __uint_as_float(u[0]) + __uint_as_float(u[1]);
+  const float s23 = __uint_as_float(w[0]) + __uint_as_float(w[1]);
+  const auto h = __builtin_amdgcn_permlane32_swap(__float_as_uint(s01), __float_as_uint(s23), false, false);
+  return __uint_as_float(h[0]) + __uint_as_float(h[1]);
+}
+// o[d] = v of lane (n, d) in every lane (n, g): __shfl(v, n + 16 d)
+__device__ __forceinline__ void rows_bcast4(float v, float o[4]) {
+  float a, b;
+  rows_pair_swap(v, a, b);
+  halves_swap(a, o[0], o[2]);
+  halves_swap(b, o[1], o[3]);
+}
+
 // write parameter p (value v) to its image position(s)
 template <bool WT = false>
 __device__ inline void mf_scatter_param(float* __restrict__ Wz, int p, float v) {

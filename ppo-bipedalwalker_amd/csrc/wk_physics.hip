@@ -1150,18 +1150,12 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool wri
         for (int d = 0; d < 4; d++) p3[d] = p3[d] + Wz[W3 + d * 64 + k] * h2;
       }
     }
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-      p3[d] = p3[d] + __shfl_xor(p3[d], 16);
-      p3[d] = p3[d] + __shfl_xor(p3[d], 32);
-    }
-    pv = pv + __shfl_xor(pv, 16);
-    pv = pv + __shfl_xor(pv, 32);
-    if (g == 0) {
-      const pf4 v = {p3[0], p3[1], p3[2], p3[3]};
-      *(pf4*)(outs + (16 * nt + n) * 8) = v;
-      outs[(16 * nt + n) * 8 + 4] = pv;
-    }
+    // the sums over the four lane groups (wk_mfma_layout.h: permlane swaps, the whole wave
+    // active); lane (n, g) holds dim g's
+    const float z3g = rows_rsum4(p3);
+    pv = rows_sum4(pv);
+    outs[(16 * nt + n) * 8 + g] = z3g;
+    if (g == 0) outs[(16 * nt + n) * 8 + 4] = pv;
   }
   wave_lds_sync();  // the outputs are written before any lane reads its walker's
   const pf4 b3 = *(const pf4*)(Wz + BA3);
@@ -1170,6 +1164,28 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool wri
   for (int d = 0; d < 4; d++) z3[d] = o[d] + b3[d];
   value = outs[wl * 8 + 4] + Wz[BC2];
   wave_lds_sync();  // outputs read before the next env-step rewrites the tile
+}
+
+// Pacing of the pair kernel's two waves per SIMD.  The SIMD arbitrates VALU issue between its two
+// co-resident waves by priority, then age (MI355X_MICROARCH.md, "Two waves per SIMD"): at equal
+// priority the older block's waves issue first, so they finished their 64 env-steps in ~25 ms
+// while the younger block's waves, left the spare slots, ran on alone for another ~14 ms at one
+// wave per SIMD (per-wave clocks, scripts/r06_wave_clock.py, profiles/r06_wave_clock.txt).  Each
+// wave publishes (launch, env-step) in its SIMD's slot once per env-step -- an atomic max from one
+// lane -- and runs at priority 1 while the slot says its partner is ahead, 0 otherwise, so the two
+// keep pace and share the SIMD to the end.  Scheduling only: no result depends on it.
+DEV void pace_partner(unsigned long long* pace, uint32_t seq, int k) {
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);  // HW_ID
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // XCC_ID[3:0]
+  const uint32_t slot = (((((xcc & 7u) * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u +
+                          ((hw >> 8) & 15u)) * 4u) + ((hw >> 4) & 3u);  // (XCC, SE, SH, CU, SIMD)
+  const unsigned long long tag = ((unsigned long long)seq << 32) | (uint32_t)k;
+  unsigned long long prev = 0;
+  if ((threadIdx.x & 63) == 0) prev = atomicMax(&pace[slot], tag);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(prev >> 32), 0);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)prev, 0);
+  if ((((unsigned long long)hi << 32) | lo) > tag) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
 }
 
 constexpr int SIDE_BLOCK = SIDE_BLOCK_THREADS;  // 4 waves: the policy's weight image is staged once per block
@@ -1244,6 +1260,7 @@ void k_env_side(EnvParams P, StepArgs A) {
 #pragma unroll 1
   for (int k = 0; k < A.k_steps; k++) {
     float a[4], lp[4], obs[12];
+    if (Q == 1 && A.pace) pace_partner(A.pace, A.pace_seq, k);
     rp_mark(rp, RP_OTHER);
     // every LDS address of the env-step derived from the thread index afresh (an opaque copy
     // made inside the loop): hoisted out of the loop they were ten loop-invariant VGPRs that

@@ -258,14 +258,8 @@ void k_ppo_grad_mfma(GradArgs ga) {
         pv = pv + wc2[Mt][r] * hc1[Mt][r];
       }
     }
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-      p3[d] = p3[d] + __shfl_xor(p3[d], 16);
-      p3[d] = p3[d] + __shfl_xor(p3[d], 32);
-    }
-    pv = pv + __shfl_xor(pv, 16);
-    pv = pv + __shfl_xor(pv, 32);
-    const float z3 = (g == 0 ? p3[0] : g == 1 ? p3[1] : g == 2 ? p3[2] : p3[3]) + b3g;
+    pv = rows_sum4(pv);
+    const float z3 = rows_rsum4(p3) + b3g;  // (lane (n, g): dim g)
     const float V = pv + bc2;
 
     // ---- PPO derivative for action dimension d = g (PPOAgent.cs:234-326) ----
@@ -285,8 +279,7 @@ void k_ppo_grad_mfma(GradArgs ga) {
     l = l * -1.0f;
     const float eo = expf(lpo);
     float zd = eo == 0.0f ? 1.0f : 0.0f;  // Matrix.HadamardDivision throws -> sample skipped
-    zd = fmaxf(zd, __shfl_xor(zd, 16));
-    zd = fmaxf(zd, __shfl_xor(zd, 32));
+    zd = rows_max4(zd);
     const bool use = valid && zd == 0.0f;
     const float lcd = l / eo;
     const float prob = expf(lp);
@@ -297,11 +290,8 @@ void k_ppo_grad_mfma(GradArgs ga) {
     const float th = mean;  // tanh(z3) again in the reference's backward pass
     const float gz3 = actorLoss * (1.0f - (th * th));
     float al[4], q[4];
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-      al[d] = __shfl(actorLoss, n + 16 * d);
-      q[d] = __shfl(gz3, n + 16 * d);
-    }
+    rows_bcast4(actorLoss, al);
+    rows_bcast4(gz3, q);
     if (g == 0) {
       diagC += criticLoss;
       diagA += use ? ((((0.0f + al[0]) + al[1]) + al[2]) + al[3]) / 4.0f : 0.0f;
@@ -685,14 +675,8 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
 #pragma unroll
           for (int r = 0; r < 4; r++) pv = __builtin_fmaf(wc2[r], hc1[M][r], pv);
         }
-#pragma unroll
-        for (int d = 0; d < 4; d++) {
-          p3[d] = p3[d] + __shfl_xor(p3[d], 16);
-          p3[d] = p3[d] + __shfl_xor(p3[d], 32);
-        }
-        pv = pv + __shfl_xor(pv, 16);
-        pv = pv + __shfl_xor(pv, 32);
-        const float z3 = (g == 0 ? p3[0] : g == 1 ? p3[1] : g == 2 ? p3[2] : p3[3]) + b3g;
+        pv = rows_sum4(pv);
+        const float z3 = rows_rsum4(p3) + b3g;  // (lane (n, g): dim g)
         const float V = pv + bc2;
         // ---- PPO derivative for action dimension d = g (PPOAgent.cs:234-326) ----
         const float act = cur.act, lpo = cur.lpo, ret = cur.ret, adv = cur.adv;
@@ -712,8 +696,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
         l = l * -1.0f;
         const float eo = expf(lpo);
         float zd = eo == 0.0f ? 1.0f : 0.0f;  // Matrix.HadamardDivision throws -> sample skipped
-        zd = fmaxf(zd, __shfl_xor(zd, 16));
-        zd = fmaxf(zd, __shfl_xor(zd, 32));
+        zd = rows_max4(zd);
         const bool use = valid && zd == 0.0f;
         const float lcd = l / eo;
         const float prob = expf(lp);
@@ -724,11 +707,8 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
         const float th = mean;  // tanh(z3) again in the reference's backward pass
         const float gz3 = actorLoss * (1.0f - (th * th));
         float al[4], q[4];
-#pragma unroll
-        for (int d = 0; d < 4; d++) {
-          al[d] = __shfl(actorLoss, n + 16 * d);
-          q[d] = __shfl(gz3, n + 16 * d);
-        }
+        rows_bcast4(actorLoss, al);
+        rows_bcast4(gz3, q);
         if (g == 0) {
           diagC += criticLoss;
           diagA += use ? ((((0.0f + al[0]) + al[1]) + al[2]) + al[3]) / 4.0f : 0.0f;
@@ -921,16 +901,20 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
   // the block fold over the four pair slabs, in pair order
   const SlabOut out(ga.partial + (size_t)blockIdx.x * SLAB);
   constexpr int NV = SLAB / 4, PER = (NV + 512 - 1) / 512;
+  // (the thread index through an opaque copy: otherwise the prologue's 16-byte offset of the
+  // weight copy is reused here and kept in scratch across the chunk loop)
+  int tf = tid;
+  asm volatile("" : "+v"(tf));
   f4 sv[PER][PAIRS];
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    const int i = tid + k * 512;
+    const int i = tf + k * 512;
 #pragma unroll
     for (int w = 0; w < PAIRS; w++) sv[k][w] = i < NV ? ((const f4*)(lds + w * SLAB))[i] : z4;
   }
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    const int i = tid + k * 512;
+    const int i = tf + k * 512;
     f4 acc = z4;
 #pragma unroll
     for (int w = 0; w < PAIRS; w++) acc = acc + sv[k][w];
@@ -1090,15 +1074,9 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
         for (int r = 0; r < 4; r++) p3[d] = __builtin_fmaf(w3[d][r], h2[r], p3[d]);
 #pragma unroll
       for (int r = 0; r < 4; r++) pv = __builtin_fmaf(wc2[r], hc1[r], pv);
-#pragma unroll
-      for (int d = 0; d < 4; d++) {
-        p3[d] = p3[d] + __shfl_xor(p3[d], 16);
-        p3[d] = p3[d] + __shfl_xor(p3[d], 32);
-      }
-      pv = pv + __shfl_xor(pv, 16);
-      pv = pv + __shfl_xor(pv, 32);
+      pv = rows_sum4(pv);
       // lane (n, g) stores dim g's partial, lanes of group 0 also V's
-      tb[O_P + w * RP + g * 16 + n] = g == 0 ? p3[0] : g == 1 ? p3[1] : g == 2 ? p3[2] : p3[3];
+      tb[O_P + w * RP + g * 16 + n] = rows_rsum4(p3);
       if (g == 0) tb[O_P + w * RP + 64 + n] = pv;
     }
     __syncthreads();  // B2: the team's partial dots
@@ -1129,8 +1107,7 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
       l = l * -1.0f;
       const float eo = expf(lpo);
       float zd = eo == 0.0f ? 1.0f : 0.0f;  // Matrix.HadamardDivision throws -> sample skipped
-      zd = fmaxf(zd, __shfl_xor(zd, 16));
-      zd = fmaxf(zd, __shfl_xor(zd, 32));
+      zd = rows_max4(zd);
       const bool use = valid && zd == 0.0f;
       const float lcd = l / eo;
       const float prob = expf(lp);
@@ -1141,12 +1118,10 @@ __global__ __launch_bounds__(256 * TEAMS) void k_ppo_grad_tp(GradArgs ga) {
       const float th = mean;  // tanh(z3) again in the reference's backward pass
       const float gz3 = actorLoss * (1.0f - (th * th));
       float q[4];
-#pragma unroll
-      for (int d = 0; d < 4; d++) q[d] = __shfl(gz3, n + 16 * d);
+      rows_bcast4(gz3, q);
       if (w == 0) {  // the sample-level terms, once per team
         float al[4];
-#pragma unroll
-        for (int d = 0; d < 4; d++) al[d] = __shfl(actorLoss, n + 16 * d);
+        rows_bcast4(actorLoss, al);
         if (g == 0) {
           diagC += criticLoss;
           diagA += use ? ((((0.0f + al[0]) + al[1]) + al[2]) + al[3]) / 4.0f : 0.0f;

@@ -61,8 +61,30 @@ __device__ __forceinline__ void rp_end(RegionProf* p) {
 struct RegionProf {};
 template <class... T>
 __device__ __forceinline__ void rp_mark(RegionProf*, int, T...) {}
+#ifdef WK_WAVE_CLOCK
+// -DWK_WAVE_CLOCK (probe builds only): every wave's start and end on the 100 MHz constant clock
+// (s_memrealtime: one clock for the whole device) with its HW_ID and XCC_ID, per launched wave
+// [start, end, hw_id, xcc_id] -- the spread of wave durations and of their ends within one launch
+static __device__ unsigned long long g_wave_clock[4 * 8192];
+#define RP_KERNEL_BEGIN(NW)                                       \
+  RegionProf* rp = nullptr;                                       \
+  const unsigned long long wc_t0_ = __builtin_amdgcn_s_memrealtime()
+#define RP_KERNEL_END()                                                                         \
+  do {                                                                                          \
+    (void)rp;                                                                                   \
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();                             \
+    const unsigned w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;                            \
+    if ((threadIdx.x & 63) == 0 && w < 8192) {                                                  \
+      g_wave_clock[4 * w] = wc_t0_;                                                             \
+      g_wave_clock[4 * w + 1] = t1;                                                             \
+      g_wave_clock[4 * w + 2] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);           \
+      g_wave_clock[4 * w + 3] = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);          \
+    }                                                                                           \
+  } while (0)
+#else
 #define RP_KERNEL_BEGIN(NW) RegionProf* rp = nullptr
 #define RP_KERNEL_END() ((void)rp)
+#endif
 #endif
 
 }  // namespace wk
@@ -79,6 +101,12 @@ __device__ __forceinline__ void rp_mark(RegionProf*, int, T...) {}
       if (hipMemcpyToSymbol(HIP_SYMBOL(wk::g_region_prof), z, sizeof(z)) != hipSuccess) return -1; \
     }                                                                                           \
     return 0;                                                                                   \
+  }
+#elif defined(WK_WAVE_CLOCK)
+#define RP_HOST_READER                                                                          \
+  extern "C" int wk_wave_clock(unsigned long long* out) {                                      \
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(wk::g_wave_clock), sizeof(unsigned long long) * 4 * 8192) \
+               == hipSuccess ? 0 : -1;                                                          \
   }
 #else
 #define RP_HOST_READER

@@ -98,3 +98,35 @@ def test_rough_offset_order_follows_the_offsets(wk, tmp_path, lanes):
     a.close()
     b.close()
 
+
+
+@pytest.mark.parametrize("rough", [0, 1])
+def test_wave_pacing_is_invisible(wk, rough):
+    """the pair kernel's pacing of its two waves per SIMD (wk_physics.hip pace_partner: per-SIMD
+    progress slots, s_setprio) only decides which co-resident wave issues first: a context
+    without it (WK_PACE=0, read at wk_create) gives the same trajectories, records and update"""
+    n, T = 40000, 16
+    cfg = dict(Horizon=T, Minibatch=n * T // 4, Epochs=1, RandomizeStart=1, RandomizeMaterial=1,
+               MaxTimesteps=30, LanesPerWalker=2, RoughFloor=rough)
+    old = os.environ.get("WK_PACE")
+    try:
+        os.environ["WK_PACE"] = "0"
+        b = wk.Engine(n, seed=SEED, **cfg)
+    finally:
+        if old is None:
+            os.environ.pop("WK_PACE")
+        else:
+            os.environ["WK_PACE"] = old
+    a = wk.Engine(n, seed=SEED, **cfg)
+    for it in range(3):
+        for e in (a, b):
+            e.rollout(T)
+        ta, tb = a.get_trajectory(T), b.get_trajectory(T)
+        for k in ta:
+            np.testing.assert_array_equal(ta[k], tb[k], err_msg=f"iteration {it}: {k}")
+        np.testing.assert_array_equal(a.get_state(), b.get_state())
+        for e in (a, b):
+            e.ppo_update(update_index=it)
+        np.testing.assert_array_equal(a.get_weights(), b.get_weights())
+    a.close()
+    b.close()
