@@ -45,6 +45,7 @@ for it in range(R + 3):
         q = np.array_split(dur, 8)
         print("   by wave-index octile (lane order), mean ms: " +
               " ".join(f"{x.mean() / 1e3:.2f}" for x in q), flush=True)
-        np.save(os.path.join(ROOT, "gpurun_out", f"wave_clock_{n}_it{it}.npy"), a)
+        tag = {"0": "unpaced", "2": "paced_nolayer"}.get(os.environ.get("WK_PACE", ""), "paced")
+        np.save(os.path.join(ROOT, "gpurun_out", f"wave_clock_{n}_{tag}_it{it}.npy"), a)
     if it < R:
         eng.ppo_update(update_index=it, sync=False)
