@@ -85,7 +85,7 @@ struct wk_ctx {
   unsigned long long* counts = nullptr;  // [WK_NEV] device (wk_count_events)
   int32_t* order = nullptr;       // [n] lane order of the split physics kernels (null: identity)
   uint32_t* order_cnt = nullptr;  // [order_cells(n)] episode-0 walkers per tile + swap count
-  unsigned long long* pace = nullptr;  // [PACE_SLOTS] the pair kernel's per-SIMD progress tags
+  unsigned long long* pace = nullptr;  // [PACE_SLOTS] per-SIMD progress tags of the env-step kernels
   uint32_t pace_seq = 0;
   // comm
   ncclComm_t comm = nullptr;
@@ -416,8 +416,9 @@ int wk_create(const wk_config* cfg, int device, int n_env, uint64_t seed, wk_ctx
       ALLOC(x->order_cnt, sizeof(uint32_t) * wk::order_cells((int)n));
     }
   }
-  // the pair kernel's pacing of co-resident waves (k_env_side); test hook WK_PACE=0: without
-  if (P.lanes == 2) {
+  // pacing of co-resident waves (k_env_side's pair mapping, k_env_step; the quad mapping runs one
+  // wave per SIMD); test hook WK_PACE=0: without
+  if (P.lanes != 4) {
     const char* o = getenv("WK_PACE");
     if (!(o && o[0] == '0')) {
       ALLOC(x->pace, sizeof(unsigned long long) * wk::PACE_SLOTS);

@@ -60,7 +60,7 @@ struct StepArgs {
   float* props;              // scene props [n][SceneDev::pstride] (k_env_scene) or null
   unsigned long long* counts;  // [NEV] event totals (counting replay, mode 4) or null
   const int32_t* order;      // k_env_side: walker of lane slot s (wk_order.hip) or null (identity)
-  // k_env_side pair mapping: per-SIMD progress tags of its two co-resident waves
+  // k_env_side pair mapping / k_env_step: per-SIMD progress tags of the co-resident waves
   // ([PACE_SLOTS], zeroed at creation; null: no pacing) and this launch's sequence number
   unsigned long long* pace;
   uint32_t pace_seq;

@@ -671,6 +671,30 @@ DEV bool state_finite(const EnvState& s) {
 // the row owns all stores.  L = 1 is the plain one-walker-per-lane mapping.
 // COUNT (one lane per walker, flat floor, given actions): the counting replay -- the same
 // physics with per-lane event counters summed into A.counts (SURVEY 8(d) F_counted).
+// Pacing of co-resident waves (k_env_side's pair mapping: two 4-wave blocks per CU; k_env_step:
+// two 64-lane blocks per SIMD).  The SIMD arbitrates VALU issue between its co-resident waves by
+// priority, then age (MI355X_MICROARCH.md, "Two waves per SIMD"): at equal priority the older
+// block's waves issue first, so in the 65,536-walker rollout they finished their 64 env-steps in
+// ~25 ms while the younger block's waves, left the spare slots, ran on alone for another ~14 ms at
+// one wave per SIMD (per-wave clocks, scripts/r06_wave_clock.py, profiles/r06_wave_clock.txt).
+// Each wave publishes (launch, env-step) in its SIMD's slot once per env-step -- an atomic max
+// from one lane -- and runs at priority 1 while the slot says another wave there is ahead, 0
+// otherwise, so the waves keep pace and share the SIMD to the end.  Scheduling only: no result
+// depends on it.
+DEV void pace_partner(unsigned long long* pace, uint32_t seq, int k) {
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);  // HW_ID
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // XCC_ID[3:0]
+  const uint32_t slot = (((((xcc & 7u) * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u +
+                          ((hw >> 8) & 15u)) * 4u) + ((hw >> 4) & 3u);  // (XCC, SE, SH, CU, SIMD)
+  const unsigned long long tag = ((unsigned long long)seq << 32) | (uint32_t)k;
+  unsigned long long prev = 0;
+  if ((threadIdx.x & 63) == 0) prev = atomicMax(&pace[slot], tag);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(prev >> 32), 0);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)prev, 0);
+  if ((((unsigned long long)hi << 32) | lo) > tag) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
 template <bool POLICY, bool RECORD, bool TRACE, int L, bool ROUGH, bool COUNT = false>
 __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArgs A) {
   static_assert(!COUNT || (L == 1 && !POLICY && !TRACE), "counting replay");
@@ -708,6 +732,7 @@ __global__ __launch_bounds__(64) WK_ENV_WPE void k_env_step(EnvParams P, StepArg
 #pragma unroll 1
   for (int k = 0; k < A.k_steps; k++) {
     float a[4], lp[4], obs[12];
+    if (A.pace) pace_partner(A.pace, A.pace_seq, k);  // (lane 0 always holds a walker)
     if (POLICY) {
       get_obs(s, obs);
       float v = 0.0f;
@@ -1164,28 +1189,6 @@ DEV void policy_mfma(const float* __restrict__ Wz, const float obs[12], bool wri
   for (int d = 0; d < 4; d++) z3[d] = o[d] + b3[d];
   value = outs[wl * 8 + 4] + Wz[BC2];
   wave_lds_sync();  // outputs read before the next env-step rewrites the tile
-}
-
-// Pacing of the pair kernel's two waves per SIMD.  The SIMD arbitrates VALU issue between its two
-// co-resident waves by priority, then age (MI355X_MICROARCH.md, "Two waves per SIMD"): at equal
-// priority the older block's waves issue first, so they finished their 64 env-steps in ~25 ms
-// while the younger block's waves, left the spare slots, ran on alone for another ~14 ms at one
-// wave per SIMD (per-wave clocks, scripts/r06_wave_clock.py, profiles/r06_wave_clock.txt).  Each
-// wave publishes (launch, env-step) in its SIMD's slot once per env-step -- an atomic max from one
-// lane -- and runs at priority 1 while the slot says its partner is ahead, 0 otherwise, so the two
-// keep pace and share the SIMD to the end.  Scheduling only: no result depends on it.
-DEV void pace_partner(unsigned long long* pace, uint32_t seq, int k) {
-  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);  // HW_ID
-  const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // XCC_ID[3:0]
-  const uint32_t slot = (((((xcc & 7u) * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u +
-                          ((hw >> 8) & 15u)) * 4u) + ((hw >> 4) & 3u);  // (XCC, SE, SH, CU, SIMD)
-  const unsigned long long tag = ((unsigned long long)seq << 32) | (uint32_t)k;
-  unsigned long long prev = 0;
-  if ((threadIdx.x & 63) == 0) prev = atomicMax(&pace[slot], tag);
-  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(prev >> 32), 0);
-  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)prev, 0);
-  if ((((unsigned long long)hi << 32) | lo) > tag) __builtin_amdgcn_s_setprio(1);
-  else __builtin_amdgcn_s_setprio(0);
 }
 
 constexpr int SIDE_BLOCK = SIDE_BLOCK_THREADS;  // 4 waves: the policy's weight image is staged once per block

@@ -20,7 +20,20 @@ eng = wk.Engine(n, seed=20250905, Horizon=64, RandomizeStart=1, Minibatch=min(n,
 lib = eng.lib
 lib.wk_wave_clock.argtypes = [C.POINTER(C.c_ulonglong)]
 buf = (C.c_ulonglong * (4 * 8192))()
+def lane_order(ep0):
+    """wk_order.hip restated: the m episode-0 walkers take the last m slots, the r-th episode-0
+    walker of the head trading places with the r-th post-reset walker of the tail"""
+    n_ = ep0.size
+    m = int(ep0.sum())
+    order = np.arange(n_)
+    h = np.flatnonzero(ep0[: n_ - m])
+    t = (n_ - m) + np.flatnonzero(~ep0[n_ - m:])
+    order[h], order[t] = t, h
+    return order
+
+
 for it in range(R + 3):
+    st0 = eng.get_state() if it >= R else None
     eng.rollout(64)
     eng.sync()
     lib.wk_wave_clock(buf)
@@ -45,7 +58,21 @@ for it in range(R + 3):
         q = np.array_split(dur, 8)
         print("   by wave-index octile (lane order), mean ms: " +
               " ".join(f"{x.mean() / 1e3:.2f}" for x in q), flush=True)
-        tag = {"0": "unpaced", "2": "paced_nolayer"}.get(os.environ.get("WK_PACE", ""), "paced")
+        tag = {"0": "unpaced", "2": "paced_nolayer"}.get(os.environ.get("WK_PACE", ""), "paced") + \
+            ("_identity" if os.environ.get("WK_ORDER") == "0" else "")
         np.save(os.path.join(ROOT, "gpurun_out", f"wave_clock_{n}_{tag}_it{it}.npy"), a)
+        if eng.rollout_mapping()["lanes_per_walker"] == 2 and os.environ.get("WK_ORDER") != "0":
+            ep0 = st0[:, 109] == 0.0
+            order = lane_order(ep0)
+            wpw = 32
+            steps = st0[order, 108].reshape(-1, wpw)
+            e0 = ep0[order].reshape(-1, wpw)
+            slow = np.argsort(dur)[-40:]
+            fast = np.argsort(dur)[:1000]
+            print(f"   episode-0 walkers {int(ep0.sum())}; slow waves: ep0/wave {e0[slow].mean(1).mean():.2f}, "
+                  f"episode steps {steps[slow].mean():.0f}; other waves holding ep0: "
+                  f"{[(int(w), round(float(dur[w]) / 1e3, 2), round(float(steps[w].mean()))) for w in np.flatnonzero(e0.any(1))[:60:4]]}",
+                  flush=True)
+            np.save(os.path.join(ROOT, "gpurun_out", f"wave_state_{n}_{tag}_it{it}.npy"), st0[order, 100:112])
     if it < R:
         eng.ppo_update(update_index=it, sync=False)

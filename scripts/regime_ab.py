@@ -30,7 +30,8 @@ for n in sizes:
             os.environ[k] = v
         eng = wk.Engine(n, seed=20250905, Horizon=T, Minibatch=min(n, 65536),
                         MinibatchGlobal=65536, RandomizeStart=1,
-                        RoughFloor=int(os.environ.get("REGIME_ROUGH", "0")))
+                        RoughFloor=int(os.environ.get("REGIME_ROUGH", "0")),
+                        LanesPerWalker=int(os.environ.get("REGIME_LANES", "0")))
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k)

@@ -100,14 +100,15 @@ def test_rough_offset_order_follows_the_offsets(wk, tmp_path, lanes):
 
 
 
-@pytest.mark.parametrize("rough", [0, 1])
-def test_wave_pacing_is_invisible(wk, rough):
-    """the pair kernel's pacing of its two waves per SIMD (wk_physics.hip pace_partner: per-SIMD
-    progress slots, s_setprio) only decides which co-resident wave issues first: a context
-    without it (WK_PACE=0, read at wk_create) gives the same trajectories, records and update"""
-    n, T = 40000, 16
+@pytest.mark.parametrize("n,lanes,rough", [(40000, 2, 0), (40000, 2, 1), (20011, 1, 0), (3000, 16, 0)])
+def test_wave_pacing_is_invisible(wk, n, lanes, rough):
+    """the pacing of co-resident waves (wk_physics.hip pace_partner: per-SIMD progress slots,
+    s_setprio; the pair kernel and k_env_step) only decides which wave of a SIMD issues first: a
+    context without it (WK_PACE=0, read at wk_create) gives the same trajectories, records and
+    update"""
+    T = 16
     cfg = dict(Horizon=T, Minibatch=n * T // 4, Epochs=1, RandomizeStart=1, RandomizeMaterial=1,
-               MaxTimesteps=30, LanesPerWalker=2, RoughFloor=rough)
+               MaxTimesteps=30, LanesPerWalker=lanes, RoughFloor=rough)
     old = os.environ.get("WK_PACE")
     try:
         os.environ["WK_PACE"] = "0"
