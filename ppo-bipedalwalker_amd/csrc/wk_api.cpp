@@ -554,7 +554,12 @@ static hipError_t launch_physics(wk_ctx* c, int mode, wk::StepArgs& A) {
     A.order = c->order;
   }
   A.pace = c->pace;
-  A.pace_seq = ++c->pace_seq;
+  if (c->pace && ++c->pace_seq == 0) {  // (2^32 launches: the tags start over, so clear the slots)
+    const hipError_t e = hipMemsetAsync(c->pace, 0, sizeof(unsigned long long) * wk::PACE_SLOTS, c->stream);
+    if (e != hipSuccess) return e;
+    c->pace_seq = 1;
+  }
+  A.pace_seq = c->pace_seq;
   return wk::launch_env_step(mode, c->P, A, c->stream);
 }
 
