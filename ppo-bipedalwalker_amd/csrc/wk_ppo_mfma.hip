@@ -84,6 +84,21 @@ DEV float row_sum16(float v) {
   return v;
 }
 
+// the sum over the 16 lanes of a DPP row, in lane 0 of the row, as ((v0 + v4) + (v8 + v12)) +
+// ((v1 + v5) + (v9 + v13)) + ... grouped ((t0 + t1) + (t2 + t3)): row_ror 12, 8, 15, 14 bring
+// lanes j + 4, j + 8, j + 1, j + 2 to lane j
+template <int CTRL>
+DEV float dpp_row(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+DEV float row_tree16(float v) {
+  v = v + dpp_row<0x12C>(v);
+  v = v + dpp_row<0x128>(v);
+  v = v + dpp_row<0x12F>(v);
+  v = v + dpp_row<0x12E>(v);
+  return v;
+}
+
 // Block slabs of the ordered reduction, written through to memory (sc1 buffer stores): the
 // kernel-end release then has no dirty slab lines to write back out of the L2, and the
 // reduction reads them from other XCDs anyway (tile-parallel kernel 12.9 -> 12.2 us per launch
@@ -493,13 +508,11 @@ enum : int {
   RT = 68, T68 = 16 * RT, RSX = 20, TSX = 16 * RSX,
   O_SX = 0, O_H1 = TSX, O_G2 = O_H1 + T68, O_GC1 = O_G2 + T68, TB = O_GC1 + T68,
   PAIRS = 4,
-  PV = 101,  // the producer's per-lane partials summed over sample lanes at the end
   LOOP_FLOATS = mf::WEND + PAIRS * 2 * TB,
   LDS_FLOATS = LOOP_FLOATS > PAIRS * SLAB ? LOOP_FLOATS : PAIRS * SLAB
 };
 static_assert(LOOP_FLOATS * 4 <= 160 * 1024, "fits the CU's LDS");
 static_assert(TB % 4 == 0 && T68 % 4 == 0 && TSX % 4 == 0, "16-byte aligned tiles");
-static_assert(PAIRS * PV * 64 <= LDS_FLOATS, "the producers' partials fit");
 }  // namespace ws
 
 __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga) {
@@ -744,24 +757,39 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
       __syncthreads();  // chunk i's tiles to the consumer; its reads of buffer (i - 1) & 1 done
     }
     __syncthreads();  // every wave is done with the weights and tiles
-    // ---- the producer's per-lane partials, raw, to R[pair][v][lane]: the whole block forms
-    // their sums over the 16 sample lanes of each row below (v order: db2, dWc2, dW3 by
-    // (d, M, r), then db3, dbc2 and the three diagnostics) ----
-    float* const R = lds + pair * (PV * 64) + lane;
+    // ---- the producer's per-lane partials summed over the 16 sample lanes of each row, in
+    // registers (row_tree16: the tree the former pass through LDS used, bit for bit), and the
+    // row's first lane writes the sum into the pair slab (v order of the old pass: db2, dWc2,
+    // dW3 by (d, M, r), db3; dbc2 and the three diagnostics from row 0 only) ----
+    float* const slab = lds + pair * SLAB;
+    const bool head = n == 0;
 #pragma unroll
     for (int M = 0; M < 4; M++)
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        R[(4 * M + r) * 64] = db2[M][r];
-        R[(16 + 4 * M + r) * 64] = awc2[M][r];
+        const float sb = row_tree16(db2[M][r]), sc = row_tree16(awc2[M][r]);
+        if (head) {
+          slab[OFF_A_B2 + 16 * M + 4 * g + r] = sb;
+          slab[OFF_C_W2 + 16 * M + 4 * g + r] = sc;
+        }
 #pragma unroll
-        for (int d = 0; d < 4; d++) R[(32 + 16 * d + 4 * M + r) * 64] = aw3[d][M][r];
+        for (int d = 0; d < 4; d++) {
+          const float sw = row_tree16(aw3[d][M][r]);
+          if (head) slab[OFF_A_W3 + d * 64 + 16 * M + 4 * g + r] = sw;
+        }
       }
-    R[96 * 64] = db3;
-    R[97 * 64] = dbc2;
-    R[98 * 64] = diagC;
-    R[99 * 64] = diagA;
-    R[100 * 64] = skipped;
+    {
+      const float s3 = row_tree16(db3), sv = row_tree16(dbc2), sC = row_tree16(diagC);
+      const float sA = row_tree16(diagA), sk = row_tree16(skipped);
+      if (head) slab[OFF_A_B3 + g] = s3;
+      if (head && g == 0) {
+        slab[OFF_C_B2] = sv;
+        slab[NPARAM] = sC;
+        slab[NPARAM + 1] = sA;
+        slab[NPARAM + 2] = sk;
+      }
+    }
+    if (lane < SLAB - (NPARAM + 3)) slab[NPARAM + 3 + lane] = 0.0f;  // (the pads)
   } else {
     // ---------------- consumer ----------------
 #pragma unroll
@@ -847,40 +875,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
       __syncthreads();
     }
     __syncthreads();  // (matches the producer's: weights and tiles are free)
-  }
-  __syncthreads();  // the producers' partials are in R
-  // ---- row sums: item (pair, v, g) = the 16 lanes of row g of partial v, four 16-byte reads
-  // and a fixed tree; at most four items per thread ----
-  constexpr int NITEM = PAIRS * PV * 4, KI = (NITEM + 511) / 512;
-  float rsum[KI];
-  int rdst[KI];
-#pragma unroll
-  for (int k = 0; k < KI; k++) {
-    const int i = tid + k * 512;
-    rdst[k] = -1;
-    rsum[k] = 0.0f;
-    if (i < NITEM) {
-      const int p = i / (PV * 4), v = (i / 4) % PV, gg = i & 3;
-      const f4* q = (const f4*)(lds + (p * PV + v) * 64 + 16 * gg);
-      const f4 t = (q[0] + q[1]) + (q[2] + q[3]);
-      rsum[k] = (t[0] + t[1]) + (t[2] + t[3]);
-      int dst;
-      if (v < 16) dst = OFF_A_B2 + 16 * (v >> 2) + 4 * gg + (v & 3);
-      else if (v < 32) dst = OFF_C_W2 + 16 * ((v - 16) >> 2) + 4 * gg + (v & 3);
-      else if (v < 96) dst = OFF_A_W3 + ((v - 32) >> 4) * 64 + 16 * (((v - 32) >> 2) & 3) + 4 * gg + (v & 3);
-      else if (v == 96) dst = OFF_A_B3 + gg;
-      else dst = gg == 0 ? (v == 97 ? OFF_C_B2 : NPARAM + (v - 98)) : -1;  // (sample terms: row 0)
-      rdst[k] = dst < 0 ? -1 : p * SLAB + dst;
-    }
-  }
-  __syncthreads();  // R is read: the pair slabs may overwrite it
-#pragma unroll
-  for (int k = 0; k < KI; k++)
-    if (rdst[k] >= 0) lds[rdst[k]] = rsum[k];
-  if (producer) {
-    if (lane < SLAB - (NPARAM + 3)) lds[pair * SLAB + NPARAM + 3 + lane] = 0.0f;  // (the pads)
-  } else {
-    float* slab = lds + pair * SLAB;
+    float* const slab = lds + pair * SLAB;
 #pragma unroll
     for (int Mj = 0; Mj < 4; Mj++)
 #pragma unroll
@@ -897,7 +892,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
         }
       }
   }
-  __syncthreads();
+  __syncthreads();  // the pair slabs are complete
   // the block fold over the four pair slabs, in pair order
   const SlabOut out(ga.partial + (size_t)blockIdx.x * SLAB);
   constexpr int NV = SLAB / 4, PER = (NV + 512 - 1) / 512;
