@@ -83,6 +83,21 @@ __device__ __forceinline__ void rows_bcast4(float v, float o[4]) {
   halves_swap(b, o[1], o[3]);
 }
 
+// the sum over the 16 lanes of a DPP row, in lane 0 of the row, as ((v0 + v4) + (v8 + v12)) +
+// ((v1 + v5) + (v9 + v13)) + ... grouped ((t0 + t1) + (t2 + t3)): row_ror 12, 8, 15, 14 bring
+// lanes j + 4, j + 8, j + 1, j + 2 to lane j
+template <int CTRL>
+__device__ __forceinline__ float dpp_row(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_tree16(float v) {
+  v = v + dpp_row<0x12C>(v);
+  v = v + dpp_row<0x128>(v);
+  v = v + dpp_row<0x12F>(v);
+  v = v + dpp_row<0x12E>(v);
+  return v;
+}
+
 // write parameter p (value v) to its image position(s)
 template <bool WT = false>
 __device__ inline void mf_scatter_param(float* __restrict__ Wz, int p, float v) {

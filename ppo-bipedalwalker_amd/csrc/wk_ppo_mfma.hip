@@ -84,21 +84,6 @@ DEV float row_sum16(float v) {
   return v;
 }
 
-// the sum over the 16 lanes of a DPP row, in lane 0 of the row, as ((v0 + v4) + (v8 + v12)) +
-// ((v1 + v5) + (v9 + v13)) + ... grouped ((t0 + t1) + (t2 + t3)): row_ror 12, 8, 15, 14 bring
-// lanes j + 4, j + 8, j + 1, j + 2 to lane j
-template <int CTRL>
-DEV float dpp_row(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-DEV float row_tree16(float v) {
-  v = v + dpp_row<0x12C>(v);
-  v = v + dpp_row<0x128>(v);
-  v = v + dpp_row<0x12F>(v);
-  v = v + dpp_row<0x12E>(v);
-  return v;
-}
-
 // Block slabs of the ordered reduction, written through to memory (sc1 buffer stores): the
 // kernel-end release then has no dirty slab lines to write back out of the L2, and the
 // reduction reads them from other XCDs anyway (tile-parallel kernel 12.9 -> 12.2 us per launch

@@ -387,6 +387,22 @@ def test_floor_face_closed_form():
     assert " 0 mismatches" in r.stdout
 
 
+def test_row_exchanges_bit_identical():
+    """The permlane / DPP lane-group exchanges (wk_mfma_layout.h rows_sum4 / rows_max4 /
+    rows_bcast4 / rows_rsum4 / row_tree16) equal the __shfl / LDS formulations they replaced, bit
+    for bit, on 67 M hashed floats incl. signed zeros and infinities (tests/cpp/rows_check.hip)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "ppo-bipedalwalker_amd", "build", "rows_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(os.path.dirname(exe)), "check"],
+                       check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 mismatches" in r.stdout
+
+
 def test_baseline_config2_physics_4096(wk, orc):
     """BASELINE config 2: 4,096 walkers, physics-step only (auto mapping: the quad split at
     this size), 10 env-steps with given actions, bit-exact vs the oracle."""
