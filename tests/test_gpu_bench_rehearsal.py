@@ -32,12 +32,19 @@ def test_bench_two_rank_rehearsal(exchange):
            "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2",
            "--steps", "2", "--warmup", "1", "--rehearse", "--walkers-global", "4096",
            "--horizon", "8", "--epochs", "1", "--regime-iters", "1", "--exchange", exchange]
+    if exchange == "ipc":
+        cmd.append("--xch-profile")  # (the exchange kernel's per-block clock split, untimed)
     p = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     assert p.returncode == 0, p.stdout[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout[-3000:]  # rank 0 only
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["scaling"] == "strong" and "rehearsal" in out
+    if exchange == "ipc":  # one split per rank: span / wait / own / gap in microseconds
+        prof = out["xch_profile_us"]
+        assert len(prof) == 2 and all(r is not None for r in prof), prof
+        for r in prof:
+            assert r["span"] > 0 and r["own"] > 0 and r["wait"] >= 0 and r["own"] <= r["span"], r
     assert out["config"]["walkers_per_gpu"] == 2048 and out["config"]["global_walkers"] == 4096
     assert out["config"]["minibatch_global"] == 4096
     assert out["config"]["exchange"] == ("ipc" if exchange == "ipc" else "host (gloo)")
