@@ -511,6 +511,23 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
   // eight waves do not sit two per SIMD, pair p = waves p and p + 4.  (The role is
   // wave-uniform in an SGPR: scalar branches, so each wave executes only its own path's
   // barriers -- both paths execute the same number.)
+  // the weight image into LDS first, by the block's first four waves (the first launched): their
+  // loads are in flight while the others launch, and the pairing barrier below publishes the image
+  // with the SIMD ids (one block barrier and one L2 round trip fewer before the first chunk)
+  if (tid < 256) {
+    constexpr int NV = WEND / 4, PER = (NV + 256 - 1) / 256;
+    f4 wv[PER];
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+      const int e = tid + i * 256;
+      if (e < NV) wv[i] = ((const f4*)ga.Wz)[e];
+    }
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+      const int e = tid + i * 256;
+      if (e < NV) ((f4*)lds)[e] = wv[i];
+    }
+  }
   __shared__ int simd_of[2 * PAIRS];
   if (lane == 0) simd_of[wave] = (int)((__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4) >> 0) & 3);
   __syncthreads();
@@ -562,22 +579,7 @@ __global__ __launch_bounds__(64 * 2 * ws::PAIRS) void k_ppo_grad_ws(GradArgs ga)
     return m;
   };
   Smp nxt;
-  if (producer) nxt = gather(c0 < nchunks ? c0 : 0);  // in flight while the weights are staged
-  {
-    constexpr int NV = WEND / 4, PER = (NV + 512 - 1) / 512;
-    f4 wv[PER];
-#pragma unroll
-    for (int i = 0; i < PER; i++) {
-      const int e = tid + i * 512;
-      if (e < NV) wv[i] = ((const f4*)ga.Wz)[e];
-    }
-#pragma unroll
-    for (int i = 0; i < PER; i++) {
-      const int e = tid + i * 512;
-      if (e < NV) ((f4*)lds)[e] = wv[i];
-    }
-  }
-  __syncthreads();
+  if (producer) nxt = gather(c0 < nchunks ? c0 : 0);
   float* const pt = lds + WEND + pair * 2 * TB;  // this pair's two tile buffers
   const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
 
