@@ -21,11 +21,12 @@
 #include "wk_mfma_layout.h"
 #include "wk_region_prof.h"
 
-// Build parts (the Makefile compiles this file seven times, in parallel): kernels are
+// Build parts (the Makefile compiles this file eight times, in parallel): kernels are
 // templates instantiated where the host shims at the end launch them, so each part holds the
-// shims of one family -- 1: the pair / quad side kernels, 5: the same on the rough floor, 2 and
-// 4: the scene-prop kernel (given actions / policy), 6 and 7: the same on the rough floor, 3: the
-// rest (1- and 16-lane kernels, the counting replay, init, obs, policy, returns).  0: all.
+// shims of one family -- 1: the pair side kernels, 8: the quad side kernels (the default
+// scheduler), 5: both on the rough floor, 2 and 4: the scene-prop kernel (given actions / policy),
+// 6 and 7: the same on the rough floor, 3: the rest (1- and 16-lane kernels, the counting replay,
+// init, obs, policy, returns).  0: all.
 #ifndef WK_PHYS_PART
 #define WK_PHYS_PART 0
 #endif
@@ -1499,7 +1500,7 @@ static void launch_lanes(int mode, const EnvParams& P, const StepArgs& A, hipStr
   if (P.rough) launch_lanes_floor<L, true>(mode, P, A, s);
   else launch_lanes_floor<L, false>(mode, P, A, s);
 }
-#if WK_PART(1) || WK_PART(5)
+#if WK_PART(1) || WK_PART(5) || WK_PART(8)
 template <int Q, bool ROUGH>
 static void launch_side(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) {
   const size_t lanes = Q == 2 ? ((size_t)P.n_env + P.wpw - 1) / P.wpw * 64 : (size_t)P.n_env * 2;
@@ -1514,6 +1515,8 @@ static void launch_side(int mode, const EnvParams& P, const StepArgs& A, hipStre
 #endif
 #if WK_PART(1)
 void launch_side_pair(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) { launch_side<1, false>(mode, P, A, s); }
+#endif
+#if WK_PART(8)  // the quad mapping: its own part, built with the default scheduler (Makefile)
 void launch_side_quad(int mode, const EnvParams& P, const StepArgs& A, hipStream_t s) { launch_side<2, false>(mode, P, A, s); }
 #endif
 #if WK_PART(5)  // RoughFloor on the pair / quad mappings (their own build part: compile time)
